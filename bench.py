@@ -1,0 +1,137 @@
+#!/usr/bin/env python3
+"""Headline benchmark: N = 32768 fp64 dense block Gauss-Jordan inversion on 1/2/4/8 MI355X.
+
+Metric (BASELINE.json): "GFLOP/s + wall-clock, N=32768 dense Gauss-Jordan at 1/2/4/8 MI355X".
+One *step* = one complete inversion of a fresh synthetic random dense N x N fp64 matrix
+(uniform [-1, 1), seeded, generated on the GPUs inside the timed region) with the block-row-cyclic
+native engine: look-ahead pivot search, chunk-pipelined RCCL pivot-row broadcast, MFMA elimination,
+final row/column permutation into the reference's distribution.  GFLOP/s uses the nominal
+inversion count 2 N^3 and is the whole-job aggregate (strong scaling: N fixed).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]            # N = 1
+    torchrun --nproc-per-node N bench.py --gpus N --steps K ...    # N > 1 (one rank per GPU, RCCL)
+
+Rank 0 prints ONE JSON line.  vs_baseline divides by the reference's own measured rate (30.8 GFLOP/s
+nominal, its best published-in-survey run: N=8192, p=8 MPI ranks, SURVEY.md §7.5 — the reference
+has no GPU path and no published N=32768 number).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REFERENCE_GFLOPS = 30.8  # reference N=8192 p=8 (35.73 s) -> 2N^3/t
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=32768)
+    ap.add_argument("--m", type=int, default=128, help="pivot block size")
+    ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
+    ap.add_argument("--gen", default="random")
+    ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--chunk-cols", type=int, default=0)
+    ap.add_argument("--no-residual", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from mpi_jordan_crazy_acceleration_amd import load_native
+
+    C = load_native()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        ids = [[C.rccl_unique_id(), C.rccl_unique_id()] if rank == 0 else None]
+        dist.broadcast_object_list(ids, src=0)
+        dev = C.hip_device(local)
+        comm = C.rccl_comm(ids[0], world, rank, local)
+    else:
+        dev = C.hip_device(local)
+        comm = C.self_comm()
+    eng = C.Engine(dev, comm, args.n, args.m, args.dtype, args.chunk_cols)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def step():
+        eng.generate(args.gen, args.seed)
+        return eng.solve()
+
+    for _ in range(args.warmup):
+        st = step()
+        if st["status"] != 0:
+            print(f"bench.py: solve failed with status {st['status']}", file=sys.stderr)
+            return 2
+    barrier()
+    t0 = time.perf_counter()
+    inner = []
+    for _ in range(args.steps):
+        st = step()
+        inner.append(st["seconds"])
+    barrier()
+    t1 = time.perf_counter()
+    ms = (t1 - t0) * 1e3 / max(args.steps, 1)
+    if world > 1:
+        t = torch.tensor([ms, max(inner)], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms, inner_max = float(t[0]), float(t[1])
+    else:
+        inner_max = max(inner)
+    res = None
+    if not args.no_residual and st["status"] == 0:
+        res = eng.residual_generated(args.gen, args.seed)
+    gflops = 2.0 * float(args.n) ** 3 / (ms / 1e3) / 1e9
+    if rank == 0:
+        out = {
+            "metric": "GFLOP/s + wall-clock, N=32768 dense Gauss-Jordan at 1/2/4/8 MI355X",
+            "value": round(gflops, 3),
+            "unit": "GFLOP/s (nominal 2N^3 per inversion, whole job)",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": round(gflops / REFERENCE_GFLOPS, 2),
+            "dtype": args.dtype,
+            "data": "synthetic: seeded uniform[-1,1) dense random matrix generated on-GPU each step",
+            "config": {
+                "model": f"dense block Gauss-Jordan inversion N={args.n} (block m={args.m}, in-place, "
+                         "min-inverse-norm block pivoting)",
+                "global_batch": 1,
+                "seq_len": args.n,
+                "parallelism": f"block-row-cyclic p={world} (RCCL over xGMI)" if world > 1 else "single GPU",
+                "n": args.n,
+                "m": args.m,
+            },
+            "solve_seconds_max": round(inner_max, 4),
+            "residual_inf": res,
+            "status": st["status"],
+            "offdiag_pivots": st["offdiag_pivots"],
+            "host_wait_ms": round(st["host_wait_ms"], 3),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

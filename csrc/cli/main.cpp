@@ -1,0 +1,170 @@
+// `gj` — command-line front end, compatible with the reference's `mpirun -np p ./a.out n m [file]`
+// (main.cpp:65-93 + the stdout contract of solve(), main.cpp:343-519).
+//
+//   gj [options] n m [file]
+//
+// Positional arguments keep the reference semantics: n and m via atoi (non-numeric or <= 0 ->
+// usage, exit 1), optional input file (text, fscanf("%lf")-compatible, or raw fp64 ".bin").
+// stdout is byte-compatible with the reference:
+//   A / corner / glob_time: %.2f / inverse matrix: + blank line / corner / residual: %e
+// Exit codes: 0 ok, 1 usage, 2 any failure.
+//
+// Options (all optional; defaults reproduce the reference on one MI355X):
+//   -p, --ranks P        number of ranks (GPUs with --device gpu, virtual ranks with --device cpu)
+//   --gpus P             alias of --ranks for GPU runs
+//   --device gpu|cpu     execution backend (default: gpu when a HIP device exists)
+//   --comm auto|rccl|loopback
+//   --dtype fp64|fp32
+//   --gen absdiff|hilbert|random|identity   generator when no file is given (reference: absdiff;
+//                        -DHILBERT -> --gen hilbert)
+//   --seed S             seed of --gen random
+//   --residual always|compat|never   compat = the reference's "p == 1!" skip (main.cpp:499-513)
+//   --print-max N        corner size (reference MAX_P = 10)
+//   --eps E              singularity threshold factor (reference EPS = 1e-15)
+//   --chunk-cols C       broadcast pipelining granularity
+//   --repeat R           time R solves, report the last (min also in --json)
+//   --out FILE           write the inverse (text, or .bin)
+//   --json               machine-readable report on stderr
+//   --sync-debug         synchronise after every phase (race screening)
+//   --wait-debugger S    sleep S seconds at start (reference -DSLEEP, main.cpp:8, :70-72)
+#include <hip/hip_runtime.h>
+#include <unistd.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "gj/io.hpp"
+#include "gj/runner.hpp"
+
+using namespace gj;
+
+static int usage(const char* prog) {
+  std::printf("usage:%s n m [<file>]\n", prog);
+  return 1;
+}
+
+static void json_report(const RunConfig& cfg, const RunReport& rep) {
+  std::fprintf(stderr,
+               "{\"n\": %lld, \"m\": %lld, \"ranks\": %d, \"device\": \"%s\", \"comm\": \"%s\", "
+               "\"dtype\": \"%s\", \"status\": %d, \"glob_time\": %.6f, \"best_time\": %.6f, "
+               "\"gflops_nominal\": %.3f, \"residual\": %.6e, \"residual_computed\": %s, "
+               "\"host_wait_ms\": %.3f, \"offdiag_pivots\": %lld}\n",
+               (long long)cfg.n, (long long)cfg.m, cfg.ranks, rep.device_desc.c_str(),
+               rep.comm_desc.c_str(), dtype_name(cfg.solve.dtype), (int)rep.status, rep.glob_time,
+               rep.best_time, rep.gflops_nominal, rep.residual,
+               rep.residual_computed ? "true" : "false", rep.stats.host_wait_ms,
+               (long long)rep.stats.offdiag_pivots);
+}
+
+int main(int argc, char* argv[]) {
+  RunConfig cfg;
+  std::vector<const char*> pos;
+  bool json = false;
+  std::string device = "auto", out_file;
+  int wait_dbg = 0;
+  for (int i = 1; i < argc; ++i) {
+    const std::string a = argv[i];
+    auto val = [&](const char* name) -> const char* {
+      if (i + 1 >= argc) {
+        std::fprintf(stderr, "%s needs a value\n", name);
+        std::exit(usage(argv[0]));
+      }
+      return argv[++i];
+    };
+    if (a.size() > 1 && a[0] == '-' && !(a[1] >= '0' && a[1] <= '9')) {
+      if (a == "-p" || a == "--ranks" || a == "--gpus") cfg.ranks = std::atoi(val(a.c_str()));
+      else if (a == "--device") device = val("--device");
+      else if (a == "--comm") cfg.comm = val("--comm");
+      else if (a == "--dtype") {
+        const std::string d = val("--dtype");
+        if (d == "fp64" || d == "f64" || d == "double") cfg.solve.dtype = DType::F64;
+        else if (d == "fp32" || d == "f32" || d == "float") cfg.solve.dtype = DType::F32;
+        else return usage(argv[0]);
+      } else if (a == "--gen") {
+        const std::string g = val("--gen");
+        if (g == "absdiff") cfg.gen.kind = GenKind::AbsDiff;
+        else if (g == "hilbert") cfg.gen.kind = GenKind::Hilbert;
+        else if (g == "random") cfg.gen.kind = GenKind::Random;
+        else if (g == "identity") cfg.gen.kind = GenKind::Identity;
+        else return usage(argv[0]);
+      } else if (a == "--seed") cfg.gen.seed = std::strtoull(val("--seed"), nullptr, 10);
+      else if (a == "--residual") {
+        const std::string r = val("--residual");
+        if (r == "always") cfg.residual = ResidualMode::Always;
+        else if (r == "compat") cfg.residual = ResidualMode::Compat;
+        else if (r == "never") cfg.residual = ResidualMode::Never;
+        else return usage(argv[0]);
+      } else if (a == "--print-max") cfg.print_max = std::atoi(val("--print-max"));
+      else if (a == "--eps") cfg.solve.eps = std::atof(val("--eps"));
+      else if (a == "--chunk-cols") cfg.solve.chunk_cols = std::atoll(val("--chunk-cols"));
+      else if (a == "--repeat") cfg.repeats = std::atoi(val("--repeat"));
+      else if (a == "--out") out_file = val("--out");
+      else if (a == "--json") json = true;
+      else if (a == "--sync-debug") cfg.solve.sync_debug = true;
+      else if (a == "--wait-debugger") wait_dbg = std::atoi(val("--wait-debugger"));
+      else if (a == "--host-threads") cfg.host_threads = std::atoi(val("--host-threads"));
+      else if (a == "--first-device") cfg.first_device = std::atoi(val("--first-device"));
+      else return usage(argv[0]);
+    } else {
+      pos.push_back(argv[i]);
+    }
+  }
+  // reference: argc in {3,4}, atoi(n) != 0, atoi(m) != 0 (main.cpp:77-83); negatives rejected too
+  if (pos.size() < 2 || pos.size() > 3) return usage(argv[0]);
+  const long long n = std::atoll(pos[0]), m = std::atoll(pos[1]);
+  if (n <= 0 || m <= 0 || cfg.ranks <= 0 || cfg.print_max < 0) return usage(argv[0]);
+  cfg.n = n;
+  cfg.m = m;
+  if (pos.size() == 3) cfg.file = pos[2];
+  if (wait_dbg > 0) sleep(wait_dbg);
+
+  if (device == "auto") {
+    int ndev = 0;
+    cfg.gpu = (hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0);
+  } else if (device == "gpu") {
+    cfg.gpu = true;
+  } else if (device == "cpu") {
+    cfg.gpu = false;
+  } else {
+    return usage(argv[0]);
+  }
+  cfg.keep_inverse = !out_file.empty();
+
+  RunReport rep;
+  try {
+    rep = run_local(cfg);
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "gj: %s\n", e.what());
+    return 2;
+  }
+  // error reporting mirrors main.cpp:372-449
+  switch (rep.status) {
+    case Status::Ok: break;
+    case Status::CannotOpen: std::printf("cannot open %s\n", cfg.file.c_str()); return 2;
+    case Status::CannotRead: std::printf("cannot read %s\n", cfg.file.c_str()); return 2;
+    case Status::NoMemory: std::printf("Not enough memory!\n"); if (!rep.message.empty()) std::fprintf(stderr, "%s\n", rep.message.c_str()); return 2;
+    case Status::Singular:
+      std::printf("A\n");
+      print_corner(stdout, rep.corner_a, (int)std::min<long long>(n, cfg.print_max));
+      std::printf("singular matrix\n");
+      if (json) json_report(cfg, rep);
+      return 2;
+    default: std::printf("error: %s\n", rep.message.c_str()); return 2;
+  }
+  std::printf("A\n");
+  print_corner(stdout, rep.corner_a, rep.nm);
+  std::printf("glob_time: %.2f\n", rep.glob_time);
+  std::printf("inverse matrix:\n\n");
+  print_corner(stdout, rep.corner_inv, rep.nm);
+  if (rep.residual_computed)
+    std::printf("residual: %e\n", rep.residual);
+  else if (cfg.residual == ResidualMode::Compat)
+    std::printf("p == 1!\n");
+  if (!out_file.empty()) write_matrix_file(out_file, n, rep.inverse.data(), n);
+  if (json) json_report(cfg, rep);
+  return 0;
+}

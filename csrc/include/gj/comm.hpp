@@ -1,0 +1,66 @@
+// Communication abstraction (replaces the reference's direct MPI calls).
+//
+// Implementations:
+//   * RcclComm     (csrc/runtime/rccl_comm.cpp)  — one RCCL communicator per stream role, over xGMI.
+//   * LoopbackComm (csrc/runtime/loopback_comm.cpp) — p "virtual ranks" as threads of one process
+//     (host or one GPU); used by the CLI's --device cpu mode and by multi-rank tests on a 1-GPU box.
+//   * PyComm       (csrc/python/module.cpp)      — trampolines into torch.distributed (gloo) so the
+//     multi-process path is testable on CPU.
+//
+// All collective calls are stream-ordered w.r.t. the Device stream role they are issued on, and
+// every rank issues them in the same program order (SPMD), exactly like the reference's blocking MPI.
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "gj/device.hpp"
+
+namespace gj {
+
+struct P2POp {
+  void* ptr;
+  size_t bytes;
+  int peer;
+  bool send;
+};
+
+class Comm {
+ public:
+  virtual ~Comm() = default;
+  virtual int size() const = 0;
+  virtual int rank() const = 0;
+  virtual std::string describe() const = 0;
+
+  // Device-memory, stream-ordered collectives.
+  virtual void allgather(Device& dev, const void* send, void* recv, size_t bytes, int s) = 0;
+  virtual void bcast(Device& dev, void* buf, size_t bytes, int root, int s) = 0;
+  virtual void allreduce_max(Device& dev, double* buf, size_t count, int s) = 0;
+  virtual void group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) = 0;
+
+  // Host-blocking helpers (once-per-run agreement: errors, timings, residual maxima).
+  virtual void barrier(Device& dev) = 0;
+  virtual double host_max(Device& dev, double v) = 0;
+  virtual void host_allgather(Device& dev, const void* send, void* recv, size_t bytes) = 0;
+};
+
+// A trivial single-rank communicator.
+class SelfComm : public Comm {
+ public:
+  int size() const override { return 1; }
+  int rank() const override { return 0; }
+  std::string describe() const override { return "self"; }
+  void allgather(Device& dev, const void* send, void* recv, size_t bytes, int s) override {
+    if (send != recv) dev.copy(recv, send, bytes, s);
+  }
+  void bcast(Device&, void*, size_t, int, int) override {}
+  void allreduce_max(Device&, double*, size_t, int) override {}
+  void group_p2p(Device&, const std::vector<P2POp>& ops, int) override {
+    GJ_REQUIRE(ops.empty(), "SelfComm: point-to-point with a peer requested");
+  }
+  void barrier(Device& dev) override { dev.sync_all(); }
+  double host_max(Device&, double v) override { return v; }
+  void host_allgather(Device&, const void* send, void* recv, size_t bytes) override;
+};
+
+}  // namespace gj

@@ -1,0 +1,88 @@
+// Concrete communicators (see gj/comm.hpp for the interface).
+#pragma once
+
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "gj/comm.hpp"
+
+namespace gj {
+
+// ---------------------------------------------------------------- RCCL over xGMI
+// One RCCL communicator per stream role that issues collectives (SIDE: pivot records and
+// once-per-run maxima; COMM: pivot-row broadcast, finalisation exchange, residual all-gather),
+// so collectives of different roles can never be reordered against each other across ranks.
+class RcclComm : public Comm {
+ public:
+  static constexpr int kIdBytes = 128;
+  static std::string unique_id();  // opaque bytes (kIdBytes)
+  // ids: one unique id per communicator (2); every rank passes the same ids.
+  RcclComm(const std::vector<std::string>& ids, int nranks, int rank, int device);
+  ~RcclComm() override;
+  int size() const override { return n_; }
+  int rank() const override { return r_; }
+  std::string describe() const override;
+
+  void allgather(Device& dev, const void* send, void* recv, size_t bytes, int s) override;
+  void bcast(Device& dev, void* buf, size_t bytes, int root, int s) override;
+  void allreduce_max(Device& dev, double* buf, size_t count, int s) override;
+  void group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) override;
+  void barrier(Device& dev) override;
+  double host_max(Device& dev, double v) override;
+  void host_allgather(Device& dev, const void* send, void* recv, size_t bytes) override;
+
+ private:
+  void* comm_for(int s) const;
+  int n_ = 1, r_ = 0, device_ = 0;
+  void* comms_[2] = {nullptr, nullptr};  // ncclComm_t
+  void* dbuf_ = nullptr;                 // small device scratch for host helpers
+  size_t dbuf_sz_ = 0;
+};
+
+// ---------------------------------------------------------------- in-process virtual ranks
+// p ranks = p threads of one process sharing a LoopbackHub.  Each collective synchronises the
+// issuing stream, meets the other ranks at a barrier and copies between their buffers (device
+// peer copies for HipDevice, memcpy for HostDevice).  Used by `gj --device cpu -p N` and by the
+// multi-rank tests that run on a single GPU.
+class LoopbackHub {
+ public:
+  explicit LoopbackHub(int p);
+  int size() const { return p_; }
+  void arrive_and_wait();
+  // published pointers / values
+  std::vector<const void*> ptr;
+  std::vector<double> val;
+  std::vector<std::vector<P2POp>> p2p;  // per source rank
+
+ private:
+  int p_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  int count_ = 0;
+  long gen_ = 0;
+};
+
+class LoopbackComm : public Comm {
+ public:
+  LoopbackComm(std::shared_ptr<LoopbackHub> hub, int rank) : hub_(std::move(hub)), r_(rank) {}
+  int size() const override { return hub_->size(); }
+  int rank() const override { return r_; }
+  std::string describe() const override { return "loopback(" + std::to_string(size()) + ")"; }
+
+  void allgather(Device& dev, const void* send, void* recv, size_t bytes, int s) override;
+  void bcast(Device& dev, void* buf, size_t bytes, int root, int s) override;
+  void allreduce_max(Device& dev, double* buf, size_t count, int s) override;
+  void group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) override;
+  void barrier(Device& dev) override;
+  double host_max(Device& dev, double v) override;
+  void host_allgather(Device& dev, const void* send, void* recv, size_t bytes) override;
+
+ private:
+  std::shared_ptr<LoopbackHub> hub_;
+  int r_;
+};
+
+}  // namespace gj

@@ -1,0 +1,110 @@
+// Device abstraction used by the solver engine.
+//
+// Two implementations exist:
+//   * HipDevice  (csrc/runtime/hip_device.hip)  — the product path: hand-written gfx950 kernels,
+//     three HIP streams (MAIN/SIDE/COMM) with priorities, event-based ordering.
+//   * HostDevice (csrc/runtime/host_device.cpp) — a plain C++ reference executor with identical
+//     semantics.  It is only ever selected explicitly (`--device cpu`, CPU tests, the reference's
+//     "512x512 single rank on CPU" plumbing config); a GPU run never falls back to it.
+//
+// Every op takes a stream role (S_MAIN/S_SIDE/S_COMM); the host device executes synchronously.
+#pragma once
+
+#include <string>
+
+#include "gj/common.hpp"
+#include "gj/layout.hpp"
+#include "gj/pivot.hpp"
+
+namespace gj {
+
+// Matrix generators (reference f / f_i, main.cpp:47-64, plus a seeded random dense generator for
+// the synthetic benchmark system).
+enum class GenKind : int { AbsDiff = 0, Hilbert = 1, Identity = 2, Random = 3, Zero = 4 };
+
+struct GenSpec {
+  GenKind kind = GenKind::AbsDiff;
+  uint64_t seed = 0;
+};
+
+// C (+)= A * B.  A is M x K and is stored either row-major (A[i*lda + k]) or "K-major"
+// (At[k*lda + i], the layout the solver keeps its multiplier panel in).
+enum class GemmOp : int { Acc = 0, Store = 1 };
+enum class ALayout : int { RowMajor = 0, KMajor = 1 };
+
+class Device {
+ public:
+  virtual ~Device() = default;
+  virtual bool on_gpu() const = 0;
+  virtual std::string describe() const = 0;
+  virtual int device_index() const { return -1; }
+
+  // ---- memory ----
+  virtual void* alloc(size_t bytes) = 0;
+  virtual void release(void* p) = 0;
+  virtual void* alloc_pinned(size_t bytes) = 0;
+  virtual void release_pinned(void* p) = 0;
+  virtual size_t free_memory() const = 0;
+  virtual void memset0(void* p, size_t bytes, int s) = 0;
+  virtual void copy(void* dst, const void* src, size_t bytes, int s) = 0;
+  virtual void copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width_bytes,
+                      size_t height, int s) = 0;
+
+  // ---- ordering ----
+  virtual int create_event(bool timing = false) = 0;
+  virtual void record(int ev, int s) = 0;
+  virtual void wait(int s, int ev) = 0;
+  virtual void sync_event(int ev) = 0;
+  virtual void sync_stream(int s) = 0;
+  virtual void sync_all() = 0;
+  virtual float event_ms(int ev_start, int ev_end) = 0;
+  virtual void* native_stream(int s) = 0;  // hipStream_t (nullptr on host)
+
+  // ---- kernels ----
+  // X (layout.rows x npad, ld npad) := A' restricted to this rank's block rows.
+  virtual void generate(DType dt, void* X, const Layout& L, GenSpec g, int s) = 0;
+  // X[r][c] := src[r][c] (doubles, ld src_ld) for r < rows, c < cols (dtype conversion).
+  virtual void upload_convert(DType dt, void* X, int64_t ldx, const double* src_dev, int64_t src_ld,
+                              int64_t rows, int64_t cols, int s) = 0;
+  // Lt[c*ldl + r] = -X[r*ldx + col0 + c]  for r < rows, c < m   (multiplier panel, K-major).
+  virtual void extract_neg_t(DType dt, void* Lt, int64_t ldl, const void* X, int64_t ldx,
+                             int64_t rows, int64_t col0, int64_t m, int s) = 0;
+  // A[i*ld + i] += alpha, i < nd.
+  virtual void add_diag(DType dt, void* A, int64_t ld, int64_t nd, double alpha, int s) = 0;
+  // For every local block row b with used[global(b)] == 0: W = -(Lt block b)^T = X[b, col-block],
+  // compute inv(W) by Gauss-Jordan with partial pivoting (reference inverse_block, main.cpp:746-820),
+  // write it transposed to inv_t[b*m*m + j*m + i] = inv(W)[i][j], its inf-norm to scores[b]
+  // (block_norm, main.cpp:669-683), and valid[b] (0 when singular: |pivot| < thresh).
+  virtual void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
+                             int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                             int s) = 0;
+  // Local argmin over this rank's candidates -> *out.
+  virtual void pivot_local(const double* scores, const int32_t* valid, const int32_t* used,
+                           const int32_t* pos, const Layout& L, PivotRec* out, int s) = 0;
+  // Global selection over p records + book-keeping (pivot_commit) -> *out.
+  virtual void pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos,
+                            int32_t* phys_at, int32_t* used, int32_t* seq, PivotResult* out,
+                            int s) = 0;
+  // R[i*ldr + j] = H[i][j] = Ht[j*m + i]   (the pivot column block of the broadcast row).
+  virtual void h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, int s) = 0;
+  // GemmOp::Acc extras (the elimination step): C columns [zc0, zc1) enter as 0, and rows
+  // [pr0, pr0 + K) are written with the corresponding rows of B instead of C + A*B (pr0 < 0: none).
+  virtual void gemm(DType dt, GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const void* A,
+                    int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int s,
+                    int64_t zc0 = 0, int64_t zc1 = 0, int64_t pr0 = -1) = 0;
+  // Finalisation gather: dst[(dst_blk[b]*m + r)*ldd + c*m + j] = X[(b*m + r)*ldx + colsrc[c]*m + j]
+  // for local block b < nblk, destination column block c < Nr.
+  virtual void permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx,
+                              int64_t nblk, int64_t m, int64_t Nr, const int32_t* dst_blk,
+                              const int32_t* colsrc, int s) = 0;
+  // out[0] = max over local real rows of sum_{j<n} |X[r][j]|  (reference norm(), main.cpp:643-667).
+  virtual void row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out,
+                           int s) = 0;
+  // out[0] = max over local real rows r of sum_{j<n} |(A_loc * Full)[r][j] - delta(global(r), j)|
+  // (matrix_mult_matrix + minus_i + norm, main.cpp:534-667, fused).  A_loc row-major ld npad,
+  // Full = the whole inverse in natural row order (npad x npad).
+  virtual void residual(DType dt, const void* A, const void* Full, const Layout& L, double* out,
+                        int s) = 0;
+};
+
+}  // namespace gj

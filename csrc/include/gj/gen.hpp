@@ -1,0 +1,41 @@
+// Matrix generators shared by the host and device executors (bitwise identical on both).
+//
+// Reference: f(i,j) = |i-j| (default) or 1/(i+j+1) under -DHILBERT, f_i = identity
+// (main.cpp:47-64).  `random` is a counter-based (stateless) uniform [-1, 1) generator so any rank
+// can produce any element without communication — the synthetic dense system of the benchmark.
+#pragma once
+
+#include "gj/common.hpp"
+#include "gj/device.hpp"
+
+namespace gj {
+
+GJ_HD inline uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// Element (i, j) of the padded matrix A' = diag(A, I) (i, j < npad).
+GJ_HD inline double gen_value(int kind, uint64_t seed, int64_t n, int64_t i, int64_t j) {
+  if (i >= n || j >= n) return (i == j) ? 1.0 : 0.0;
+  switch (kind) {
+    case 0: {  // AbsDiff
+      const int64_t d = i - j;
+      return (double)(d < 0 ? -d : d);
+    }
+    case 1:  // Hilbert
+      return 1.0 / (double)(i + j + 1);
+    case 2:  // Identity
+      return (i == j) ? 1.0 : 0.0;
+    case 3: {  // Random uniform [-1, 1)
+      const uint64_t h = splitmix64(seed * 0x2545F4914F6CDD1Dull ^ ((uint64_t)i << 32) ^ (uint64_t)j);
+      return (double)(h >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+    }
+    default:  // Zero
+      return 0.0;
+  }
+}
+
+}  // namespace gj

@@ -1,0 +1,73 @@
+// HipDevice — the MI355X execution backend (csrc/runtime/hip_device.cpp).
+#pragma once
+
+#include <vector>
+
+#include "gj/device.hpp"
+
+namespace gj {
+
+class HipDevice : public Device {
+ public:
+  explicit HipDevice(int device_index);
+  ~HipDevice() override;
+  bool on_gpu() const override { return true; }
+  std::string describe() const override;
+  int device_index() const override { return dev_; }
+
+  void* alloc(size_t bytes) override;
+  void release(void* p) override;
+  void* alloc_pinned(size_t bytes) override;
+  void release_pinned(void* p) override;
+  size_t free_memory() const override;
+  void memset0(void* p, size_t bytes, int s) override;
+  void copy(void* dst, const void* src, size_t bytes, int s) override;
+  void copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width_bytes,
+              size_t height, int s) override;
+
+  int create_event(bool timing = false) override;
+  void record(int ev, int s) override;
+  void wait(int s, int ev) override;
+  void sync_event(int ev) override;
+  void sync_stream(int s) override;
+  void sync_all() override;
+  float event_ms(int ev_start, int ev_end) override;
+  void* native_stream(int s) override;
+
+  void generate(DType dt, void* X, const Layout& L, GenSpec g, int s) override;
+  void upload_convert(DType dt, void* X, int64_t ldx, const double* src_dev, int64_t src_ld,
+                      int64_t rows, int64_t cols, int s) override;
+  void extract_neg_t(DType dt, void* Lt, int64_t ldl, const void* X, int64_t ldx, int64_t rows,
+                     int64_t col0, int64_t m, int s) override;
+  void add_diag(DType dt, void* A, int64_t ld, int64_t nd, double alpha, int s) override;
+  void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
+                     int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                     int s) override;
+  void pivot_local(const double* scores, const int32_t* valid, const int32_t* used,
+                   const int32_t* pos, const Layout& L, PivotRec* out, int s) override;
+  void pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos, int32_t* phys_at,
+                    int32_t* used, int32_t* seq, PivotResult* out, int s) override;
+  void h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, int s) override;
+  void gemm(DType dt, GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const void* A,
+            int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int s, int64_t zc0 = 0,
+            int64_t zc1 = 0, int64_t pr0 = -1) override;
+  void permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx, int64_t nblk,
+                      int64_t m, int64_t Nr, const int32_t* dst_blk, const int32_t* colsrc,
+                      int s) override;
+  void row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out,
+                   int s) override;
+  void residual(DType dt, const void* A, const void* Full, const Layout& L, double* out,
+                int s) override;
+
+ private:
+  void* scratch(size_t bytes, int slot);
+  void activate() const;
+
+  int dev_ = 0;
+  void* streams_[kNumStreams] = {nullptr, nullptr, nullptr};
+  std::vector<void*> events_;
+  void* scratch_[2] = {nullptr, nullptr};
+  size_t scratch_sz_[2] = {0, 0};
+};
+
+}  // namespace gj

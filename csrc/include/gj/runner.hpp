@@ -1,0 +1,50 @@
+// In-process driver: one host thread per rank (GPU or virtual host rank), the reference's solve()
+// flow (main.cpp:343-519): allocate -> read/generate A -> print A -> time the inversion -> print
+// inverse -> recompute A -> residual.  Shared by the `gj` CLI and the Python bindings.
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "gj/engine.hpp"
+
+namespace gj {
+
+enum class ResidualMode : int { Never = 0, Always = 1, Compat = 2 };
+
+struct RunConfig {
+  int64_t n = 0, m = 0;
+  int ranks = 1;
+  bool gpu = true;
+  std::string comm = "auto";        // auto | rccl | loopback
+  int first_device = 0;
+  GenSpec gen;
+  std::string file;                 // input file (text or .bin); empty => generator
+  const double* input = nullptr;    // or a caller-owned n x n row-major matrix
+  SolveOptions solve;
+  ResidualMode residual = ResidualMode::Always;
+  int print_max = kDefaultPrintMax;
+  bool want_corners = true;
+  bool keep_inverse = false;        // gather the full inverse into RunReport::inverse
+  int host_threads = 0;
+  int repeats = 1;                  // timed solves (the last one is reported; min kept too)
+};
+
+struct RunReport {
+  Status status = Status::Ok;
+  std::string message;
+  double glob_time = 0;             // max over ranks (reference glob_time, main.cpp:455-458)
+  double best_time = 0;             // min over repeats of glob_time
+  bool residual_computed = false;
+  double residual = 0;
+  int nm = 0;
+  std::vector<double> corner_a, corner_inv;
+  std::vector<double> inverse;      // n*n if keep_inverse
+  SolveStats stats;                 // rank 0
+  std::string device_desc, comm_desc;
+  double gflops_nominal = 0;        // 2 n^3 / glob_time / 1e9
+};
+
+RunReport run_local(const RunConfig& cfg);
+
+}  // namespace gj

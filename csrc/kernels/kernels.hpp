@@ -1,0 +1,50 @@
+// Launch wrappers of the hand-written gfx950 kernels (implemented in csrc/kernels/*.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "gj/common.hpp"
+#include "gj/layout.hpp"
+#include "gj/pivot.hpp"
+
+namespace gj {
+namespace kern {
+
+// gemm.hip
+void gemm(DType dt, int op /*0 acc, 1 store*/, int a_kmajor, int64_t M, int64_t N, int64_t K,
+          const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
+          hipStream_t s, int64_t zc0 = 0, int64_t zc1 = 0, int64_t pr0 = -1);
+int residual_nparts(int64_t N);
+void residual_partial(DType dt, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                      const void* B, int64_t ldb, int64_t n_real, int64_t blk_m, int64_t p,
+                      int64_t k, double* partial, hipStream_t s);
+
+// blockinv.hip
+void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
+                   int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                   hipStream_t s, void* scratch, int* iscratch);
+// scratch needed by the generic (m > 256) path
+size_t block_inverse_scratch_bytes(DType dt, const Layout& L);
+size_t block_inverse_iscratch_bytes(const Layout& L);
+
+// misc.hip
+void generate(DType dt, void* X, const Layout& L, int kind, uint64_t seed, hipStream_t s);
+void upload_convert(DType dt, void* X, int64_t ldx, const double* src, int64_t src_ld, int64_t rows,
+                    int64_t cols, hipStream_t s);
+void extract_neg_t(DType dt, void* Lt, int64_t ldl, const void* X, int64_t ldx, int64_t rows,
+                   int64_t col0, int64_t m, hipStream_t s);
+void add_diag(DType dt, void* A, int64_t ld, int64_t nd, double alpha, hipStream_t s);
+void pivot_local(const double* scores, const int32_t* valid, const int32_t* used, const int32_t* pos,
+                 const Layout& L, PivotRec* out, hipStream_t s);
+void pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos, int32_t* phys_at,
+                  int32_t* used, int32_t* seq, PivotResult* out, hipStream_t s);
+void h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, hipStream_t s);
+void permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx, int64_t nblk,
+                    int64_t m, int64_t Nr, const int32_t* dst_blk, const int32_t* colsrc,
+                    hipStream_t s);
+void row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out, hipStream_t s);
+// reduce residual partials: out = max over real local rows of sum_parts partial[r][*]
+void residual_reduce(const double* partial, int nparts, const Layout& L, double* out, hipStream_t s);
+
+}  // namespace kern
+}  // namespace gj

@@ -1,0 +1,316 @@
+// Memory-bound helper kernels of the engine (gfx950).
+//
+//   generate        <- init_matrix / f / f_i            (main.cpp:47-64, :128-149)
+//   extract_neg_t   <- get(a, E, i, t) of the hot loop  (main.cpp:690-708, :1172) — here one tiled
+//                      transpose of block column t into the K-major multiplier panel
+//   pivot_local     <- local candidate scan             (main.cpp:1039-1066)
+//   pivot_global    <- pivot_op over all ranks          (main.cpp:729-744, :1074)
+//   permute_blocks  <- the row swaps (main.cpp:1100-1131) done once at the end
+//   row_abs_max     <- norm()                           (main.cpp:643-667)
+//   residual_reduce <- norm() of the residual strip     (main.cpp:494-507)
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "gj/gen.hpp"
+#include "kernels.hpp"
+
+namespace gj {
+namespace kern {
+
+namespace {
+inline unsigned grid_for(int64_t work, int per_block, int64_t cap = 1 << 20) {
+  int64_t g = (work + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+// atomic max for non-negative doubles: their IEEE bit patterns order like the values
+__device__ inline void atomic_max_nonneg(double* addr, double v) {
+  if (!(v >= 0.0)) v = __longlong_as_double(0x7ff8000000000000ll);  // NaN propagates as max
+  atomicMax(reinterpret_cast<unsigned long long*>(addr), (unsigned long long)__double_as_longlong(v));
+}
+}  // namespace
+
+// ---------------------------------------------------------------- generate
+template <typename T>
+__global__ void generate_kernel(T* X, int64_t rows, int64_t npad, int64_t n, int64_t m, int64_t p,
+                                int64_t k, int kind, uint64_t seed) {
+  const int64_t total = rows * npad;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / npad, j = e - r * npad;
+    const int64_t gr = ((r / m) * p + k) * m + r % m;
+    X[e] = (T)gen_value(kind, seed, n, gr, j);
+  }
+}
+
+void generate(DType dt, void* X, const Layout& L, int kind, uint64_t seed, hipStream_t s) {
+  const int64_t total = L.rows * L.npad;
+  if (total <= 0) return;
+  const unsigned grid = grid_for(total, 256 * 4);
+  if (dt == DType::F64)
+    hipLaunchKernelGGL(generate_kernel<double>, dim3(grid), dim3(256), 0, s, static_cast<double*>(X),
+                       L.rows, L.npad, L.n, L.m, L.p, L.k, kind, seed);
+  else
+    hipLaunchKernelGGL(generate_kernel<float>, dim3(grid), dim3(256), 0, s, static_cast<float*>(X),
+                       L.rows, L.npad, L.n, L.m, L.p, L.k, kind, seed);
+}
+
+// ---------------------------------------------------------------- upload_convert
+template <typename T>
+__global__ void upload_kernel(T* X, int64_t ldx, const double* src, int64_t ld, int64_t rows,
+                              int64_t cols) {
+  const int64_t total = rows * cols;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / cols, j = e - r * cols;
+    X[r * ldx + j] = (T)src[r * ld + j];
+  }
+}
+
+void upload_convert(DType dt, void* X, int64_t ldx, const double* src, int64_t src_ld, int64_t rows,
+                    int64_t cols, hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return;
+  const unsigned grid = grid_for(rows * cols, 256 * 4);
+  if (dt == DType::F64)
+    hipLaunchKernelGGL(upload_kernel<double>, dim3(grid), dim3(256), 0, s, static_cast<double*>(X),
+                       ldx, src, src_ld, rows, cols);
+  else
+    hipLaunchKernelGGL(upload_kernel<float>, dim3(grid), dim3(256), 0, s, static_cast<float*>(X), ldx,
+                       src, src_ld, rows, cols);
+}
+
+// ---------------------------------------------------------------- extract_neg_t (tiled transpose)
+template <typename T>
+__global__ __launch_bounds__(256) void extract_kernel(T* __restrict__ Lt, int64_t ldl,
+                                                      const T* __restrict__ X, int64_t ldx,
+                                                      int64_t rows, int64_t col0, int64_t m) {
+  __shared__ T tile[64][65];
+  const int64_t r0 = (int64_t)blockIdx.x * 64, c0 = (int64_t)blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int i = ty + 4 * q;
+    const int64_t r = r0 + i, c = c0 + tx;
+    tile[i][tx] = (r < rows && c < m) ? X[r * ldx + col0 + c] : T(0);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int j = ty + 4 * q;
+    const int64_t c = c0 + j, r = r0 + tx;
+    if (r < rows && c < m) Lt[c * ldl + r] = -tile[tx][j];
+  }
+}
+
+void extract_neg_t(DType dt, void* Lt, int64_t ldl, const void* X, int64_t ldx, int64_t rows,
+                   int64_t col0, int64_t m, hipStream_t s) {
+  if (rows <= 0 || m <= 0) return;
+  dim3 grid((unsigned)((rows + 63) / 64), (unsigned)((m + 63) / 64));
+  if (dt == DType::F64)
+    hipLaunchKernelGGL(extract_kernel<double>, grid, dim3(256), 0, s, static_cast<double*>(Lt), ldl,
+                       static_cast<const double*>(X), ldx, rows, col0, m);
+  else
+    hipLaunchKernelGGL(extract_kernel<float>, grid, dim3(256), 0, s, static_cast<float*>(Lt), ldl,
+                       static_cast<const float*>(X), ldx, rows, col0, m);
+}
+
+// ---------------------------------------------------------------- add_diag / h_block
+template <typename T>
+__global__ void add_diag_kernel(T* A, int64_t ld, int64_t nd, double alpha) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nd) A[i * ld + i] += (T)alpha;
+}
+
+void add_diag(DType dt, void* A, int64_t ld, int64_t nd, double alpha, hipStream_t s) {
+  if (nd <= 0) return;
+  const unsigned grid = grid_for(nd, 256);
+  if (dt == DType::F64)
+    hipLaunchKernelGGL(add_diag_kernel<double>, dim3(grid), dim3(256), 0, s, static_cast<double*>(A),
+                       ld, nd, alpha);
+  else
+    hipLaunchKernelGGL(add_diag_kernel<float>, dim3(grid), dim3(256), 0, s, static_cast<float*>(A), ld,
+                       nd, alpha);
+}
+
+template <typename T>
+__global__ void h_block_kernel(T* R, int64_t ldr, const T* Ht, int64_t m) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= m * m) return;
+  const int64_t i = e / m, j = e - i * m;
+  R[i * ldr + j] = Ht[j * m + i];
+}
+
+void h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, hipStream_t s) {
+  const unsigned grid = grid_for(m * m, 256);
+  if (dt == DType::F64)
+    hipLaunchKernelGGL(h_block_kernel<double>, dim3(grid), dim3(256), 0, s, static_cast<double*>(R), ldr,
+                       static_cast<const double*>(Ht), m);
+  else
+    hipLaunchKernelGGL(h_block_kernel<float>, dim3(grid), dim3(256), 0, s, static_cast<float*>(R), ldr,
+                       static_cast<const float*>(Ht), m);
+}
+
+// ---------------------------------------------------------------- pivot selection
+__global__ __launch_bounds__(256) void pivot_local_kernel(const double* scores, const int32_t* valid,
+                                                          const int32_t* used, const int32_t* pos,
+                                                          int64_t nblk, int64_t p, int64_t k,
+                                                          PivotRec* out) {
+  __shared__ PivotRec sh[256];
+  PivotRec best = pivot_invalid();
+  for (int64_t b = threadIdx.x; b < nblk; b += 256) {
+    const int64_t g = b * p + k;
+    if (used[g] || !valid[b]) continue;
+    PivotRec c;
+    c.score = scores[b];
+    c.logical = pos[g];
+    c.phys = (int32_t)g;
+    c.valid = 1;
+    c.pad_ = 0;
+    if (pivot_better(c, best, (int32_t)p)) best = c;
+  }
+  sh[threadIdx.x] = best;
+  __syncthreads();
+  for (int off = 128; off >= 1; off >>= 1) {
+    if ((int)threadIdx.x < off) {
+      const PivotRec o = sh[threadIdx.x + off];
+      if (pivot_better(o, sh[threadIdx.x], (int32_t)p)) sh[threadIdx.x] = o;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = sh[0];
+}
+
+void pivot_local(const double* scores, const int32_t* valid, const int32_t* used, const int32_t* pos,
+                 const Layout& L, PivotRec* out, hipStream_t s) {
+  hipLaunchKernelGGL(pivot_local_kernel, dim3(1), dim3(256), 0, s, scores, valid, used, pos, L.nblk,
+                     L.p, L.k, out);
+}
+
+__global__ void pivot_global_kernel(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos,
+                                    int32_t* phys_at, int32_t* used, int32_t* seq, PivotResult* out) {
+  if (threadIdx.x != 0) return;
+  PivotRec best = pivot_invalid();
+  for (int32_t q = 0; q < p; ++q)
+    if (pivot_better(recs[q], best, p)) best = recs[q];
+  PivotResult r;
+  r.step = t;
+  r.pad_ = 0;
+  if (best.valid) {
+    r.found = 1;
+    r.phys = best.phys;
+    r.owner = best.phys % p;
+    r.logical = best.logical;
+    r.score = best.score;
+    pivot_commit(t, best.phys, pos, phys_at, used, seq);
+  } else {
+    r.found = 0;
+    r.phys = -1;
+    r.owner = -1;
+    r.logical = -1;
+    r.score = 0.0;
+  }
+  *out = r;
+}
+
+void pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos, int32_t* phys_at,
+                  int32_t* used, int32_t* seq, PivotResult* out, hipStream_t s) {
+  hipLaunchKernelGGL(pivot_global_kernel, dim3(1), dim3(64), 0, s, recs, p, t, pos, phys_at, used, seq,
+                     out);
+}
+
+// ---------------------------------------------------------------- permute_blocks
+template <typename T>
+__global__ __launch_bounds__(256) void permute_kernel(T* __restrict__ dst, int64_t ldd,
+                                                      const T* __restrict__ X, int64_t ldx, int m,
+                                                      int64_t ncols, const int32_t* dst_blk,
+                                                      const int32_t* colsrc) {
+  const int64_t row = blockIdx.x;  // local row of X
+  const int64_t b = row / m, r = row - b * m;
+  T* d = dst + ((int64_t)dst_blk[b] * m + r) * ldd;
+  const T* s = X + row * ldx;
+  for (int64_t col = (int64_t)blockIdx.y * 1024 + threadIdx.x; col < ncols;
+       col += (int64_t)gridDim.y * 1024) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t cc = col + u * 256;
+      if (cc < ncols) {
+        const int c = (int)(cc / m), j = (int)(cc - (int64_t)c * m);
+        d[cc] = s[(int64_t)colsrc[c] * m + j];
+      }
+    }
+  }
+}
+
+void permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx, int64_t nblk,
+                    int64_t m, int64_t Nr, const int32_t* dst_blk, const int32_t* colsrc,
+                    hipStream_t s) {
+  if (nblk <= 0) return;
+  const int64_t ncols = Nr * m;
+  const unsigned gy = (unsigned)std::min<int64_t>((ncols + 1023) / 1024, 64);
+  dim3 grid((unsigned)(nblk * m), gy);
+  if (dt == DType::F64)
+    hipLaunchKernelGGL(permute_kernel<double>, grid, dim3(256), 0, s, static_cast<double*>(dst), ldd,
+                       static_cast<const double*>(X), ldx, (int)m, ncols, dst_blk, colsrc);
+  else
+    hipLaunchKernelGGL(permute_kernel<float>, grid, dim3(256), 0, s, static_cast<float*>(dst), ldd,
+                       static_cast<const float*>(X), ldx, (int)m, ncols, dst_blk, colsrc);
+}
+
+// ---------------------------------------------------------------- norms
+template <typename T>
+__global__ __launch_bounds__(256) void row_abs_kernel(const T* X, int64_t ldx, int64_t n, int64_t m,
+                                                      int64_t p, int64_t k, double* out) {
+  const int64_t r = blockIdx.x;
+  const int64_t gr = ((r / m) * p + k) * m + r % m;
+  if (gr >= n) return;
+  double s = 0.0;
+  for (int64_t j = threadIdx.x; j < n; j += 256) s += fabs((double)X[r * ldx + j]);
+  __shared__ double sh[4];
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomic_max_nonneg(out, sh[0] + sh[1] + sh[2] + sh[3]);
+}
+
+void row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out, hipStream_t s) {
+  (void)hipMemsetAsync(out, 0, sizeof(double), s);
+  if (L.rows <= 0) return;
+  if (dt == DType::F64)
+    hipLaunchKernelGGL(row_abs_kernel<double>, dim3((unsigned)L.rows), dim3(256), 0, s,
+                       static_cast<const double*>(X), ldx, L.n, L.m, L.p, L.k, out);
+  else
+    hipLaunchKernelGGL(row_abs_kernel<float>, dim3((unsigned)L.rows), dim3(256), 0, s,
+                       static_cast<const float*>(X), ldx, L.n, L.m, L.p, L.k, out);
+}
+
+__global__ __launch_bounds__(256) void residual_reduce_kernel(const double* partial, int nparts,
+                                                              int64_t rows, int64_t n, int64_t m,
+                                                              int64_t p, int64_t k, double* out) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  double s = 0.0;
+  bool real = false;
+  if (r < rows) {
+    const int64_t gr = ((r / m) * p + k) * m + r % m;
+    real = gr < n;
+    if (real)
+      for (int q = 0; q < nparts; ++q) s += partial[r * nparts + q];
+  }
+  double v = real ? s : 0.0;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+  if ((threadIdx.x & 63) == 0) atomic_max_nonneg(out, v);
+}
+
+void residual_reduce(const double* partial, int nparts, const Layout& L, double* out, hipStream_t s) {
+  (void)hipMemsetAsync(out, 0, sizeof(double), s);
+  if (L.rows <= 0) return;
+  hipLaunchKernelGGL(residual_reduce_kernel, dim3((unsigned)((L.rows + 255) / 256)), dim3(256), 0, s,
+                     partial, nparts, L.rows, L.n, L.m, L.p, L.k, out);
+}
+
+}  // namespace kern
+}  // namespace gj

@@ -1,0 +1,365 @@
+// Python bindings (pybind11) of the native framework: devices, communicators, the engine and the
+// in-process runner.  The module is built in-tree as mpi_jordan_crazy_acceleration_amd/_C*.so and
+// shares the HIP runtime / RCCL already loaded by torch (the package imports torch first).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <memory>
+
+#include "gj/comms.hpp"
+#include "gj/engine.hpp"
+#include "gj/hip_device.hpp"
+#include "gj/host_device.hpp"
+#include "gj/io.hpp"
+#include "gj/runner.hpp"
+
+namespace py = pybind11;
+using namespace gj;
+
+namespace {
+
+DType parse_dtype(const std::string& s) {
+  if (s == "fp64" || s == "float64" || s == "f64" || s == "double") return DType::F64;
+  if (s == "fp32" || s == "float32" || s == "f32" || s == "float") return DType::F32;
+  throw std::invalid_argument("dtype must be fp64 or fp32");
+}
+
+GenKind parse_gen(const std::string& s) {
+  if (s == "absdiff") return GenKind::AbsDiff;
+  if (s == "hilbert") return GenKind::Hilbert;
+  if (s == "identity") return GenKind::Identity;
+  if (s == "random") return GenKind::Random;
+  if (s == "zero") return GenKind::Zero;
+  throw std::invalid_argument("unknown generator " + s);
+}
+
+// Communicator implemented in Python (torch.distributed, gloo) — host memory only.
+class PyComm : public Comm {
+ public:
+  PyComm(py::object impl, int rank, int size) : impl_(std::move(impl)), r_(rank), n_(size) {}
+  int size() const override { return n_; }
+  int rank() const override { return r_; }
+  std::string describe() const override { return "python(" + std::to_string(n_) + ")"; }
+  void allgather(Device& dev, const void* send, void* recv, size_t bytes, int) override {
+    check(dev);
+    py::gil_scoped_acquire g;
+    impl_.attr("allgather")((uintptr_t)send, (uintptr_t)recv, bytes);
+  }
+  void bcast(Device& dev, void* buf, size_t bytes, int root, int) override {
+    check(dev);
+    py::gil_scoped_acquire g;
+    impl_.attr("bcast")((uintptr_t)buf, bytes, root);
+  }
+  void allreduce_max(Device& dev, double* buf, size_t count, int) override {
+    check(dev);
+    py::gil_scoped_acquire g;
+    impl_.attr("allreduce_max")((uintptr_t)buf, count);
+  }
+  void group_p2p(Device& dev, const std::vector<P2POp>& ops, int) override {
+    check(dev);
+    py::gil_scoped_acquire g;
+    py::list l;
+    for (const auto& op : ops) l.append(py::make_tuple((uintptr_t)op.ptr, op.bytes, op.peer, op.send));
+    impl_.attr("group_p2p")(l);
+  }
+  void barrier(Device&) override {
+    py::gil_scoped_acquire g;
+    impl_.attr("barrier")();
+  }
+  double host_max(Device&, double v) override {
+    py::gil_scoped_acquire g;
+    return impl_.attr("host_max")(v).cast<double>();
+  }
+  void host_allgather(Device&, const void* send, void* recv, size_t bytes) override {
+    py::gil_scoped_acquire g;
+    impl_.attr("allgather")((uintptr_t)send, (uintptr_t)recv, bytes);
+  }
+
+ private:
+  static void check(Device& dev) {
+    if (dev.on_gpu()) throw std::runtime_error("PyComm works on host memory only (use RcclComm on GPUs)");
+  }
+  py::object impl_;
+  int r_, n_;
+};
+
+py::dict stats_to_dict(const SolveStats& st) {
+  py::dict d;
+  d["status"] = (int)st.status;
+  d["singular_step"] = st.singular_step;
+  d["seconds"] = st.seconds;
+  d["host_wait_ms"] = st.host_wait_ms;
+  d["pivots"] = st.pivots;
+  d["offdiag_pivots"] = st.offdiag_pivots;
+  d["bcast_bytes"] = st.bcast_bytes;
+  return d;
+}
+
+py::array_t<double> to_array(const std::vector<double>& v, int64_t r, int64_t c) {
+  py::array_t<double> a({r, c});
+  if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), sizeof(double) * r * c);
+  return a;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, mod) {
+  mod.doc() = "MI355X-native block Gauss-Jordan inversion: native engine, HIP kernels, RCCL comm";
+
+  mod.def("version", [] { return std::string("0.1.0"); });
+  mod.def("device_count", [] {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+  });
+  mod.def("rccl_unique_id", [] { return py::bytes(RcclComm::unique_id()); });
+
+  // Kernel-level entry points (raw pointers; used by the per-kernel numerics tests and
+  // mpi_jordan_crazy_acceleration_amd.ops).  Every op runs on the MAIN stream and is waited for.
+  using U = uintptr_t;
+  auto lay = [](int64_t n, int64_t m, int64_t p, int64_t k) { return Layout::make(n, m, p, k); };
+  py::class_<Device, std::shared_ptr<Device>>(mod, "Device")
+      .def_property_readonly("on_gpu", &Device::on_gpu)
+      .def("describe", &Device::describe)
+      .def("sync", &Device::sync_all, py::call_guard<py::gil_scoped_release>())
+      .def("gemm",
+           [](Device& d, const std::string& dt, const std::string& op, bool a_kmajor, int64_t M,
+              int64_t N, int64_t K, U A, int64_t lda, U B, int64_t ldb, U C, int64_t ldc, int64_t zc0,
+              int64_t zc1, int64_t pr0) {
+             d.gemm(parse_dtype(dt), op == "store" ? GemmOp::Store : GemmOp::Acc,
+                    a_kmajor ? ALayout::KMajor : ALayout::RowMajor, M, N, K, (const void*)A, lda,
+                    (const void*)B, ldb, (void*)C, ldc, S_MAIN, zc0, zc1, pr0);
+             d.sync_stream(S_MAIN);
+           },
+           py::arg("dtype"), py::arg("op"), py::arg("a_kmajor"), py::arg("M"), py::arg("N"), py::arg("K"),
+           py::arg("A"), py::arg("lda"), py::arg("B"), py::arg("ldb"), py::arg("C"), py::arg("ldc"),
+           py::arg("zc0") = 0, py::arg("zc1") = 0, py::arg("pr0") = -1)
+      .def("generate",
+           [lay](Device& d, const std::string& dt, U X, int64_t n, int64_t m, int64_t p, int64_t k,
+                 const std::string& kind, uint64_t seed) {
+             GenSpec g;
+             g.kind = parse_gen(kind);
+             g.seed = seed;
+             d.generate(parse_dtype(dt), (void*)X, lay(n, m, p, k), g, S_MAIN);
+             d.sync_stream(S_MAIN);
+           })
+      .def("extract_neg_t",
+           [](Device& d, const std::string& dt, U Lt, int64_t ldl, U X, int64_t ldx, int64_t rows,
+              int64_t col0, int64_t m) {
+             d.extract_neg_t(parse_dtype(dt), (void*)Lt, ldl, (const void*)X, ldx, rows, col0, m, S_MAIN);
+             d.sync_stream(S_MAIN);
+           })
+      .def("block_inverse",
+           [lay](Device& d, const std::string& dt, U Lt, int64_t ldl, U inv_t, U scores, U valid,
+                 U used, int64_t n, int64_t m, int64_t p, int64_t k, double thresh) {
+             d.block_inverse(parse_dtype(dt), (const void*)Lt, ldl, (void*)inv_t, (double*)scores,
+                             (int32_t*)valid, (const int32_t*)used, lay(n, m, p, k), thresh, S_MAIN);
+             d.sync_stream(S_MAIN);
+           })
+      .def("permute_blocks",
+           [](Device& d, const std::string& dt, U dst, int64_t ldd, U X, int64_t ldx, int64_t nblk,
+              int64_t m, int64_t Nr, U dst_blk, U colsrc) {
+             d.permute_blocks(parse_dtype(dt), (void*)dst, ldd, (const void*)X, ldx, nblk, m, Nr,
+                              (const int32_t*)dst_blk, (const int32_t*)colsrc, S_MAIN);
+             d.sync_stream(S_MAIN);
+           })
+      .def("row_abs_max",
+           [lay](Device& d, const std::string& dt, U X, int64_t ldx, int64_t n, int64_t m, int64_t p,
+                 int64_t k, U out) {
+             d.row_abs_max(parse_dtype(dt), (const void*)X, ldx, lay(n, m, p, k), (double*)out, S_MAIN);
+             d.sync_stream(S_MAIN);
+           })
+      .def("residual",
+           [lay](Device& d, const std::string& dt, U A, U Full, int64_t n, int64_t m, int64_t p,
+                 int64_t k, U out) {
+             d.residual(parse_dtype(dt), (const void*)A, (const void*)Full, lay(n, m, p, k),
+                        (double*)out, S_MAIN);
+             d.sync_stream(S_MAIN);
+           });
+  mod.def("hip_device", [](int idx) { return std::shared_ptr<Device>(new HipDevice(idx)); });
+  mod.def("host_device", [](int nthreads) { return std::shared_ptr<Device>(new HostDevice(nthreads)); },
+          py::arg("nthreads") = 0);
+
+  py::class_<Comm, std::shared_ptr<Comm>>(mod, "Comm")
+      .def_property_readonly("size", &Comm::size)
+      .def_property_readonly("rank", &Comm::rank)
+      .def("describe", &Comm::describe);
+  mod.def("self_comm", [] { return std::shared_ptr<Comm>(new SelfComm()); });
+  mod.def("rccl_comm",
+          [](std::vector<py::bytes> ids, int nranks, int rank, int device) {
+            std::vector<std::string> s;
+            for (auto& b : ids) s.push_back(std::string(b));
+            py::gil_scoped_release rel;
+            return std::shared_ptr<Comm>(new RcclComm(s, nranks, rank, device));
+          });
+  mod.def("py_comm", [](py::object impl, int rank, int size) {
+    return std::shared_ptr<Comm>(new PyComm(std::move(impl), rank, size));
+  });
+
+  // Engine keeps its device and communicator alive.
+  struct PyEngine {
+    std::shared_ptr<Device> dev;
+    std::shared_ptr<Comm> comm;
+    std::unique_ptr<Engine> eng;
+  };
+  py::class_<PyEngine>(mod, "Engine")
+      .def(py::init([](std::shared_ptr<Device> dev, std::shared_ptr<Comm> comm, int64_t n, int64_t m,
+                       const std::string& dtype, int64_t chunk_cols, double eps, bool sync_debug) {
+             SolveOptions o;
+             o.dtype = parse_dtype(dtype);
+             o.chunk_cols = chunk_cols;
+             o.eps = eps;
+             o.sync_debug = sync_debug;
+             auto* pe = new PyEngine();
+             pe->dev = dev;
+             pe->comm = comm;
+             pe->eng.reset(new Engine(*dev, *comm, n, m, o));
+             return pe;
+           }),
+           py::arg("device"), py::arg("comm"), py::arg("n"), py::arg("m"), py::arg("dtype") = "fp64",
+           py::arg("chunk_cols") = 0, py::arg("eps") = kDefaultEps, py::arg("sync_debug") = false)
+      .def_property_readonly("layout",
+                             [](PyEngine& e) {
+                               const Layout& L = e.eng->layout();
+                               py::dict d;
+                               d["n"] = L.n; d["m"] = L.m; d["p"] = L.p; d["k"] = L.k;
+                               d["Nr"] = L.Nr; d["npad"] = L.npad; d["nblk"] = L.nblk;
+                               d["rows"] = L.rows; d["real_rows"] = e.eng->real_local_rows();
+                               return d;
+                             })
+      .def("generate",
+           [](PyEngine& e, const std::string& kind, uint64_t seed) {
+             GenSpec g;
+             g.kind = parse_gen(kind);
+             g.seed = seed;
+             py::gil_scoped_release rel;
+             e.eng->generate(g);
+           },
+           py::arg("kind") = "absdiff", py::arg("seed") = 0)
+      .def("upload_local_rows",
+           [](PyEngine& e, py::array_t<double, py::array::c_style | py::array::forcecast> a) {
+             const int64_t real = e.eng->real_local_rows(), n = e.eng->layout().n;
+             if (a.ndim() != 2 || a.shape(0) != real || a.shape(1) != n)
+               throw std::invalid_argument("expected (real_rows, n) float64 array");
+             const double* p = a.data();
+             py::gil_scoped_release rel;
+             e.eng->upload_local_rows(p, n);
+           })
+      .def("input_panel_ptr", [](PyEngine& e) { return (uintptr_t)e.eng->input_panel(); })
+      .def("result_panel_ptr", [](PyEngine& e) { return (uintptr_t)e.eng->result_panel(); })
+      .def("norm_inf", [](PyEngine& e) {
+        py::gil_scoped_release rel;
+        return e.eng->norm_inf();
+      })
+      .def("solve", [](PyEngine& e) {
+        SolveStats st;
+        {
+          py::gil_scoped_release rel;
+          st = e.eng->solve();
+        }
+        return stats_to_dict(st);
+      })
+      .def("download_local_rows", [](PyEngine& e) {
+        const int64_t real = e.eng->real_local_rows(), n = e.eng->layout().n;
+        py::array_t<double> a({real, n});
+        double* p = a.mutable_data();
+        {
+          py::gil_scoped_release rel;
+          e.eng->download_local_rows(p, n);
+        }
+        return a;
+      })
+      .def("corner", [](PyEngine& e, int nm, int which) {
+        std::vector<double> c;
+        {
+          py::gil_scoped_release rel;
+          c = e.eng->corner(nm, which);
+        }
+        return to_array(c, nm, nm);
+      })
+      .def("residual_generated",
+           [](PyEngine& e, const std::string& kind, uint64_t seed) {
+             GenSpec g;
+             g.kind = parse_gen(kind);
+             g.seed = seed;
+             py::gil_scoped_release rel;
+             return e.eng->residual_generated(g);
+           },
+           py::arg("kind") = "absdiff", py::arg("seed") = 0)
+      .def("residual_rows", [](PyEngine& e, py::array_t<double, py::array::c_style | py::array::forcecast> a) {
+        const int64_t real = e.eng->real_local_rows(), n = e.eng->layout().n;
+        if (a.ndim() != 2 || a.shape(0) != real || a.shape(1) != n)
+          throw std::invalid_argument("expected (real_rows, n) float64 array");
+        const double* p = a.data();
+        py::gil_scoped_release rel;
+        return e.eng->residual_rows(p, n);
+      });
+
+  mod.def("run_local", [](py::dict d) {
+    RunConfig c;
+    c.n = d["n"].cast<int64_t>();
+    c.m = d["m"].cast<int64_t>();
+    if (d.contains("ranks")) c.ranks = d["ranks"].cast<int>();
+    if (d.contains("device")) c.gpu = d["device"].cast<std::string>() == "gpu";
+    if (d.contains("comm")) c.comm = d["comm"].cast<std::string>();
+    if (d.contains("gen")) c.gen.kind = parse_gen(d["gen"].cast<std::string>());
+    if (d.contains("seed")) c.gen.seed = d["seed"].cast<uint64_t>();
+    if (d.contains("file")) c.file = d["file"].cast<std::string>();
+    if (d.contains("dtype")) c.solve.dtype = parse_dtype(d["dtype"].cast<std::string>());
+    if (d.contains("chunk_cols")) c.solve.chunk_cols = d["chunk_cols"].cast<int64_t>();
+    if (d.contains("eps")) c.solve.eps = d["eps"].cast<double>();
+    if (d.contains("sync_debug")) c.solve.sync_debug = d["sync_debug"].cast<bool>();
+    if (d.contains("residual")) {
+      const std::string r = d["residual"].cast<std::string>();
+      c.residual = r == "never" ? ResidualMode::Never : r == "compat" ? ResidualMode::Compat : ResidualMode::Always;
+    }
+    if (d.contains("print_max")) c.print_max = d["print_max"].cast<int>();
+    if (d.contains("keep_inverse")) c.keep_inverse = d["keep_inverse"].cast<bool>();
+    if (d.contains("host_threads")) c.host_threads = d["host_threads"].cast<int>();
+    if (d.contains("repeats")) c.repeats = d["repeats"].cast<int>();
+    py::array_t<double, py::array::c_style | py::array::forcecast> inp;
+    if (d.contains("input") && !d["input"].is_none()) {
+      inp = d["input"].cast<py::array_t<double, py::array::c_style | py::array::forcecast>>();
+      if (inp.ndim() != 2 || inp.shape(0) != c.n || inp.shape(1) != c.n)
+        throw std::invalid_argument("input must be (n, n)");
+      c.input = inp.data();
+    }
+    RunReport r;
+    {
+      py::gil_scoped_release rel;
+      r = run_local(c);
+    }
+    py::dict o;
+    o["status"] = (int)r.status;
+    o["message"] = r.message;
+    o["glob_time"] = r.glob_time;
+    o["best_time"] = r.best_time;
+    o["residual_computed"] = r.residual_computed;
+    o["residual"] = r.residual;
+    o["nm"] = r.nm;
+    o["corner_a"] = to_array(r.corner_a, r.corner_a.empty() ? 0 : r.nm, r.corner_a.empty() ? 0 : r.nm);
+    o["corner_inv"] = to_array(r.corner_inv, r.corner_inv.empty() ? 0 : r.nm, r.corner_inv.empty() ? 0 : r.nm);
+    if (c.keep_inverse && r.status == Status::Ok) o["inverse"] = to_array(r.inverse, c.n, c.n);
+    o["stats"] = stats_to_dict(r.stats);
+    o["device"] = r.device_desc;
+    o["comm"] = r.comm_desc;
+    o["gflops_nominal"] = r.gflops_nominal;
+    return o;
+  });
+
+  mod.def("read_matrix_file", [](const std::string& path, int64_t n) {
+    std::vector<double> v;
+    Status s;
+    {
+      py::gil_scoped_release rel;
+      s = read_matrix_file(path, n, v);
+    }
+    if (s == Status::CannotOpen) throw std::runtime_error("cannot open " + path);
+    if (s == Status::CannotRead) throw std::runtime_error("cannot read " + path);
+    return to_array(v, n, n);
+  });
+}

@@ -1,0 +1,215 @@
+// HipDevice: HIP runtime side of the MI355X backend — streams, events, HBM allocation and kernel
+// dispatch into csrc/kernels/*.hip.
+//
+// Streams: MAIN (trailing update, normal priority), SIDE (look-ahead pivot search, highest
+// priority) and COMM (normalise + broadcast, highest priority).  All three are non-blocking w.r.t.
+// the legacy default stream.  Nothing in the step loop ever calls hipDeviceSynchronize; the host
+// only blocks on the 32-byte pivot result of the SIDE stream.
+#include "gj/hip_device.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+#include "../kernels/kernels.hpp"
+
+namespace gj {
+
+#define HIP_OK(expr)                                                                         \
+  do {                                                                                       \
+    hipError_t e_ = (expr);                                                                  \
+    if (e_ != hipSuccess)                                                                    \
+      throw Error(e_ == hipErrorOutOfMemory ? Status::NoMemory : Status::CommError,          \
+                  std::string("HIP error ") + hipGetErrorString(e_) + " at " + __FILE__ + ":" + \
+                      std::to_string(__LINE__) + " (" #expr ")");                            \
+  } while (0)
+
+static inline hipStream_t hs(void* p) { return static_cast<hipStream_t>(p); }
+
+HipDevice::HipDevice(int device_index) : dev_(device_index) {
+  int ndev = 0;
+  HIP_OK(hipGetDeviceCount(&ndev));
+  GJ_REQUIRE(device_index >= 0 && device_index < ndev, "HIP device index out of range");
+  activate();
+  int lo = 0, hi = 0;
+  HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  for (int s = 0; s < kNumStreams; ++s) {
+    hipStream_t st;
+    const int prio = (s == S_MAIN) ? lo : hi;
+    HIP_OK(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, prio));
+    streams_[s] = st;
+  }
+}
+
+HipDevice::~HipDevice() {
+  activate();
+  hipDeviceSynchronize();
+  for (void* e : events_) hipEventDestroy(static_cast<hipEvent_t>(e));
+  for (void* s : streams_)
+    if (s) hipStreamDestroy(hs(s));
+  for (void* p : scratch_)
+    if (p) hipFree(p);
+}
+
+void HipDevice::activate() const { hipSetDevice(dev_); }
+
+std::string HipDevice::describe() const {
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev_) != hipSuccess) return "hip:" + std::to_string(dev_);
+  return std::string("hip:") + std::to_string(dev_) + " " + prop.gcnArchName + " (" +
+         std::to_string(prop.multiProcessorCount) + " CUs, " +
+         std::to_string(prop.totalGlobalMem >> 30) + " GiB)";
+}
+
+void* HipDevice::alloc(size_t bytes) {
+  activate();
+  void* p = nullptr;
+  HIP_OK(hipMalloc(&p, bytes ? bytes : 64));
+  return p;
+}
+void HipDevice::release(void* p) {
+  activate();
+  hipFree(p);
+}
+void* HipDevice::alloc_pinned(size_t bytes) {
+  void* p = nullptr;
+  HIP_OK(hipHostMalloc(&p, bytes ? bytes : 64, hipHostMallocDefault));
+  return p;
+}
+void HipDevice::release_pinned(void* p) { hipHostFree(p); }
+size_t HipDevice::free_memory() const {
+  activate();
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 0;
+  return fr;
+}
+void HipDevice::memset0(void* p, size_t bytes, int s) {
+  if (bytes) HIP_OK(hipMemsetAsync(p, 0, bytes, hs(streams_[s])));
+}
+void HipDevice::copy(void* dst, const void* src, size_t bytes, int s) {
+  if (bytes && dst != src)
+    HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, hs(streams_[s])));
+}
+void HipDevice::copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t w, size_t h,
+                       int s) {
+  if (w && h) HIP_OK(hipMemcpy2DAsync(dst, dpitch, src, spitch, w, h, hipMemcpyDefault, hs(streams_[s])));
+}
+
+int HipDevice::create_event(bool timing) {
+  activate();
+  hipEvent_t e;
+  HIP_OK(hipEventCreateWithFlags(&e, timing ? hipEventDefault : hipEventDisableTiming));
+  events_.push_back(e);
+  return (int)events_.size() - 1;
+}
+void HipDevice::record(int ev, int s) {
+  HIP_OK(hipEventRecord(static_cast<hipEvent_t>(events_[ev]), hs(streams_[s])));
+}
+void HipDevice::wait(int s, int ev) {
+  HIP_OK(hipStreamWaitEvent(hs(streams_[s]), static_cast<hipEvent_t>(events_[ev]), 0));
+}
+void HipDevice::sync_event(int ev) { HIP_OK(hipEventSynchronize(static_cast<hipEvent_t>(events_[ev]))); }
+void HipDevice::sync_stream(int s) { HIP_OK(hipStreamSynchronize(hs(streams_[s]))); }
+void HipDevice::sync_all() {
+  for (int s = 0; s < kNumStreams; ++s) sync_stream(s);
+}
+float HipDevice::event_ms(int a, int b) {
+  float ms = 0.f;
+  HIP_OK(hipEventElapsedTime(&ms, static_cast<hipEvent_t>(events_[a]), static_cast<hipEvent_t>(events_[b])));
+  return ms;
+}
+void* HipDevice::native_stream(int s) { return streams_[s]; }
+
+void* HipDevice::scratch(size_t bytes, int slot) {
+  if (bytes > scratch_sz_[slot]) {
+    activate();
+    sync_all();
+    if (scratch_[slot]) hipFree(scratch_[slot]);
+    scratch_[slot] = nullptr;
+    HIP_OK(hipMalloc(&scratch_[slot], bytes));
+    scratch_sz_[slot] = bytes;
+  }
+  return scratch_[slot];
+}
+
+static void check_launch() {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw Error(Status::CommError, std::string("kernel launch failed: ") + hipGetErrorString(e));
+}
+
+void HipDevice::generate(DType dt, void* X, const Layout& L, GenSpec g, int s) {
+  kern::generate(dt, X, L, (int)g.kind, g.seed, hs(streams_[s]));
+  check_launch();
+}
+void HipDevice::upload_convert(DType dt, void* X, int64_t ldx, const double* src, int64_t src_ld,
+                               int64_t rows, int64_t cols, int s) {
+  kern::upload_convert(dt, X, ldx, src, src_ld, rows, cols, hs(streams_[s]));
+  check_launch();
+}
+void HipDevice::extract_neg_t(DType dt, void* Lt, int64_t ldl, const void* X, int64_t ldx,
+                              int64_t rows, int64_t col0, int64_t m, int s) {
+  kern::extract_neg_t(dt, Lt, ldl, X, ldx, rows, col0, m, hs(streams_[s]));
+  check_launch();
+}
+void HipDevice::add_diag(DType dt, void* A, int64_t ld, int64_t nd, double alpha, int s) {
+  kern::add_diag(dt, A, ld, nd, alpha, hs(streams_[s]));
+  check_launch();
+}
+void HipDevice::block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
+                              int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                              int s) {
+  void* sc = nullptr;
+  int* isc = nullptr;
+  const size_t b1 = kern::block_inverse_scratch_bytes(dt, L);
+  if (b1) {
+    sc = scratch(b1, 0);
+    isc = static_cast<int*>(scratch(kern::block_inverse_iscratch_bytes(L), 1));
+  }
+  kern::block_inverse(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, hs(streams_[s]), sc, isc);
+  check_launch();
+}
+void HipDevice::pivot_local(const double* scores, const int32_t* valid, const int32_t* used,
+                            const int32_t* pos, const Layout& L, PivotRec* out, int s) {
+  kern::pivot_local(scores, valid, used, pos, L, out, hs(streams_[s]));
+  check_launch();
+}
+void HipDevice::pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos,
+                             int32_t* phys_at, int32_t* used, int32_t* seq, PivotResult* out,
+                             int s) {
+  kern::pivot_global(recs, p, t, pos, phys_at, used, seq, out, hs(streams_[s]));
+  check_launch();
+}
+void HipDevice::h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, int s) {
+  kern::h_block(dt, R, ldr, Ht, m, hs(streams_[s]));
+  check_launch();
+}
+void HipDevice::gemm(DType dt, GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const void* A,
+                     int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int s,
+                     int64_t zc0, int64_t zc1, int64_t pr0) {
+  kern::gemm(dt, op == GemmOp::Acc ? 0 : 1, al == ALayout::KMajor ? 1 : 0, M, N, K, A, lda, B, ldb,
+             C, ldc, hs(streams_[s]), zc0, zc1, pr0);
+  check_launch();
+}
+void HipDevice::permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx,
+                               int64_t nblk, int64_t m, int64_t Nr, const int32_t* dst_blk,
+                               const int32_t* colsrc, int s) {
+  kern::permute_blocks(dt, dst, ldd, X, ldx, nblk, m, Nr, dst_blk, colsrc, hs(streams_[s]));
+  check_launch();
+}
+void HipDevice::row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out,
+                            int s) {
+  kern::row_abs_max(dt, X, ldx, L, out, hs(streams_[s]));
+  check_launch();
+}
+void HipDevice::residual(DType dt, const void* A, const void* Full, const Layout& L, double* out,
+                         int s) {
+  const int nparts = kern::residual_nparts(L.npad);
+  double* partial = static_cast<double*>(scratch(sizeof(double) * (size_t)L.rows * nparts, 0));
+  kern::residual_partial(dt, L.rows, L.npad, L.npad, A, L.npad, Full, L.npad, L.n, L.m, L.p, L.k,
+                         partial, hs(streams_[s]));
+  check_launch();
+  kern::residual_reduce(partial, nparts, L, out, hs(streams_[s]));
+  check_launch();
+}
+
+}  // namespace gj

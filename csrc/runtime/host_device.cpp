@@ -1,0 +1,340 @@
+// HostDevice: plain C++ reference executor of the Device interface.
+//
+// Used for `gj --device cpu` (the reference's CPU-only "plumbing" configuration), for CPU tests of
+// the distributed protocol, and as an oracle.  It is never chosen implicitly for a GPU run.
+// Streams/events are no-ops: every op completes before it returns.
+#include "gj/host_device.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "gj/gen.hpp"
+
+namespace gj {
+
+namespace {
+
+template <typename F>
+void parallel_for(int64_t n, int nthreads, F f) {
+  if (n <= 0) return;
+  int nt = (int)std::min<int64_t>(nthreads, n);
+  if (nt <= 1) {
+    for (int64_t i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(nt);
+  for (int w = 0; w < nt; ++w)
+    th.emplace_back([=, &f] {
+      for (int64_t i = w; i < n; i += nt) f(i);
+    });
+  for (auto& t : th) t.join();
+}
+
+template <typename T>
+T* tp(void* p) {
+  return static_cast<T*>(p);
+}
+template <typename T>
+const T* tp(const void* p) {
+  return static_cast<const T*>(p);
+}
+
+template <typename T>
+void gemm_t(GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const T* A, int64_t lda,
+            const T* B, int64_t ldb, T* C, int64_t ldc, int nthreads, int64_t zc0, int64_t zc1,
+            int64_t pr0) {
+  parallel_for(M, nthreads, [&](int64_t i) {
+    if (op == GemmOp::Acc && pr0 >= 0 && i >= pr0 && i < pr0 + K) {
+      for (int64_t j = 0; j < N; ++j) C[i * ldc + j] = B[(i - pr0) * ldb + j];
+      return;
+    }
+    std::vector<double> acc(N, 0.0);
+    for (int64_t k = 0; k < K; ++k) {
+      const double a = (al == ALayout::RowMajor) ? (double)A[i * lda + k] : (double)A[k * lda + i];
+      if (a == 0.0) continue;
+      const T* b = B + k * ldb;
+      for (int64_t j = 0; j < N; ++j) acc[j] += a * (double)b[j];
+    }
+    T* c = C + i * ldc;
+    if (op == GemmOp::Acc)
+      for (int64_t j = 0; j < N; ++j)
+        c[j] = (T)((j >= zc0 && j < zc1 ? 0.0 : (double)c[j]) + acc[j]);
+    else
+      for (int64_t j = 0; j < N; ++j) c[j] = (T)acc[j];
+  });
+}
+
+// In-place Gauss-Jordan sweep on W (m x m, row-major) with partial pivoting over not-yet-used rows.
+// Returns false when singular (|pivot| < thresh).  prow[k] = pivot row of column k.
+template <typename T>
+bool sweep_inverse(std::vector<double>& W, int64_t m, double thresh, std::vector<int64_t>& prow) {
+  std::vector<char> used(m, 0);
+  for (int64_t k = 0; k < m; ++k) {
+    int64_t r = -1;
+    double best = -1.0;
+    for (int64_t i = 0; i < m; ++i)
+      if (!used[i] && std::fabs(W[i * m + k]) > best) {
+        best = std::fabs(W[i * m + k]);
+        r = i;
+      }
+    if (!(best >= thresh)) return false;  // also catches NaN
+    used[r] = 1;
+    prow[k] = r;
+    const double inv = 1.0 / W[r * m + k];
+    for (int64_t j = 0; j < m; ++j) W[r * m + j] *= inv;
+    W[r * m + k] = inv;
+    for (int64_t i = 0; i < m; ++i) {
+      if (i == r) continue;
+      const double f = W[i * m + k];
+      if (f == 0.0) continue;
+      for (int64_t j = 0; j < m; ++j) W[i * m + j] -= f * W[r * m + j];
+      W[i * m + k] = -f * inv;
+    }
+  }
+  return true;
+}
+
+}  // namespace
+
+HostDevice::HostDevice(int nthreads) {
+  nthreads_ = nthreads > 0 ? nthreads : (int)std::max(1u, std::thread::hardware_concurrency());
+}
+
+std::string HostDevice::describe() const {
+  return "host(" + std::to_string(nthreads_) + " threads)";
+}
+
+void* HostDevice::alloc(size_t bytes) {
+  void* p = nullptr;
+  if (posix_memalign(&p, 64, std::max<size_t>(bytes, 64)) != 0 || !p)
+    throw Error(Status::NoMemory, "host allocation failed");
+  return p;
+}
+void HostDevice::release(void* p) { std::free(p); }
+void* HostDevice::alloc_pinned(size_t bytes) { return alloc(bytes); }
+void HostDevice::release_pinned(void* p) { std::free(p); }
+size_t HostDevice::free_memory() const { return ~size_t(0); }
+void HostDevice::memset0(void* p, size_t bytes, int) { std::memset(p, 0, bytes); }
+void HostDevice::copy(void* dst, const void* src, size_t bytes, int) {
+  if (dst != src) std::memmove(dst, src, bytes);
+}
+void HostDevice::copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t w, size_t h,
+                        int) {
+  for (size_t r = 0; r < h; ++r)
+    std::memmove(static_cast<char*>(dst) + r * dpitch, static_cast<const char*>(src) + r * spitch, w);
+}
+
+int HostDevice::create_event(bool) { return nev_++; }
+void HostDevice::record(int, int) {}
+void HostDevice::wait(int, int) {}
+void HostDevice::sync_event(int) {}
+void HostDevice::sync_stream(int) {}
+void HostDevice::sync_all() {}
+float HostDevice::event_ms(int, int) { return 0.f; }
+
+void HostDevice::generate(DType dt, void* X, const Layout& L, GenSpec g, int) {
+  parallel_for(L.rows, nthreads_, [&](int64_t r) {
+    const int64_t gr = L.global_row(r);
+    for (int64_t j = 0; j < L.npad; ++j) {
+      const double v = gen_value((int)g.kind, g.seed, L.n, gr, j);
+      if (dt == DType::F64)
+        tp<double>(X)[r * L.npad + j] = v;
+      else
+        tp<float>(X)[r * L.npad + j] = (float)v;
+    }
+  });
+}
+
+void HostDevice::upload_convert(DType dt, void* X, int64_t ldx, const double* src, int64_t src_ld,
+                                int64_t rows, int64_t cols, int) {
+  for (int64_t r = 0; r < rows; ++r)
+    for (int64_t j = 0; j < cols; ++j) {
+      if (dt == DType::F64)
+        tp<double>(X)[r * ldx + j] = src[r * src_ld + j];
+      else
+        tp<float>(X)[r * ldx + j] = (float)src[r * src_ld + j];
+    }
+}
+
+void HostDevice::extract_neg_t(DType dt, void* Lt, int64_t ldl, const void* X, int64_t ldx,
+                               int64_t rows, int64_t col0, int64_t m, int) {
+  for (int64_t r = 0; r < rows; ++r)
+    for (int64_t c = 0; c < m; ++c) {
+      if (dt == DType::F64)
+        tp<double>(Lt)[c * ldl + r] = -tp<double>(X)[r * ldx + col0 + c];
+      else
+        tp<float>(Lt)[c * ldl + r] = -tp<float>(X)[r * ldx + col0 + c];
+    }
+}
+
+void HostDevice::add_diag(DType dt, void* A, int64_t ld, int64_t nd, double alpha, int) {
+  for (int64_t i = 0; i < nd; ++i) {
+    if (dt == DType::F64)
+      tp<double>(A)[i * ld + i] += alpha;
+    else
+      tp<float>(A)[i * ld + i] += (float)alpha;
+  }
+}
+
+void HostDevice::block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
+                               int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                               int) {
+  const int64_t m = L.m;
+  parallel_for(L.nblk, nthreads_, [&](int64_t b) {
+    const int64_t g = L.global_block(b);
+    if (used[g]) {
+      valid[b] = 0;
+      scores[b] = 0;
+      return;
+    }
+    std::vector<double> W(m * m);
+    for (int64_t i = 0; i < m; ++i)
+      for (int64_t j = 0; j < m; ++j)
+        W[i * m + j] = (dt == DType::F64) ? -tp<double>(Lt)[j * ldl + b * m + i]
+                                          : -(double)tp<float>(Lt)[j * ldl + b * m + i];
+    std::vector<int64_t> prow(m);
+    const bool ok = sweep_inverse<double>(W, m, thresh, prow);
+    if (!ok) {
+      valid[b] = 0;
+      scores[b] = 0;
+      return;
+    }
+    double sc = 0.0;
+    for (int64_t i = 0; i < m; ++i) {
+      double s = 0.0;
+      for (int64_t j = 0; j < m; ++j) s += std::fabs(W[i * m + j]);
+      sc = std::max(sc, s);
+    }
+    valid[b] = std::isfinite(sc) ? 1 : 0;
+    scores[b] = sc;
+    // Y[k][prow[u]] = W[prow[k]][u]; inv_t[j*m + i] = Y[i][j]
+    for (int64_t k = 0; k < m; ++k)
+      for (int64_t u = 0; u < m; ++u) {
+        const double y = W[prow[k] * m + u];
+        const int64_t idx = b * m * m + prow[u] * m + k;
+        if (dt == DType::F64)
+          tp<double>(inv_t)[idx] = y;
+        else
+          tp<float>(inv_t)[idx] = (float)y;
+      }
+  });
+}
+
+void HostDevice::pivot_local(const double* scores, const int32_t* valid, const int32_t* used,
+                             const int32_t* pos, const Layout& L, PivotRec* out, int) {
+  PivotRec best = pivot_invalid();
+  for (int64_t b = 0; b < L.nblk; ++b) {
+    const int64_t g = L.global_block(b);
+    if (used[g] || !valid[b]) continue;
+    PivotRec c;
+    c.score = scores[b];
+    c.logical = pos[g];
+    c.phys = (int32_t)g;
+    c.valid = 1;
+    c.pad_ = 0;
+    if (pivot_better(c, best, (int32_t)L.p)) best = c;
+  }
+  *out = best;
+}
+
+void HostDevice::pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos,
+                              int32_t* phys_at, int32_t* used, int32_t* seq, PivotResult* out, int) {
+  PivotRec best = pivot_invalid();
+  for (int32_t q = 0; q < p; ++q)
+    if (pivot_better(recs[q], best, p)) best = recs[q];
+  PivotResult r{};
+  r.step = t;
+  if (best.valid) {
+    r.found = 1;
+    r.phys = best.phys;
+    r.owner = best.phys % p;
+    r.logical = best.logical;
+    r.score = best.score;
+    pivot_commit(t, best.phys, pos, phys_at, used, seq);
+  } else {
+    r.found = 0;
+    r.phys = -1;
+    r.owner = -1;
+    r.logical = -1;
+  }
+  *out = r;
+}
+
+void HostDevice::h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, int) {
+  for (int64_t i = 0; i < m; ++i)
+    for (int64_t j = 0; j < m; ++j) {
+      if (dt == DType::F64)
+        tp<double>(R)[i * ldr + j] = tp<double>(Ht)[j * m + i];
+      else
+        tp<float>(R)[i * ldr + j] = tp<float>(Ht)[j * m + i];
+    }
+}
+
+void HostDevice::gemm(DType dt, GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K,
+                      const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
+                      int, int64_t zc0, int64_t zc1, int64_t pr0) {
+  if (M <= 0 || N <= 0) return;
+  if (dt == DType::F64)
+    gemm_t<double>(op, al, M, N, K, tp<double>(A), lda, tp<double>(B), ldb, tp<double>(C), ldc,
+                   nthreads_, zc0, zc1, pr0);
+  else
+    gemm_t<float>(op, al, M, N, K, tp<float>(A), lda, tp<float>(B), ldb, tp<float>(C), ldc,
+                  nthreads_, zc0, zc1, pr0);
+}
+
+void HostDevice::permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx,
+                                int64_t nblk, int64_t m, int64_t Nr, const int32_t* dst_blk,
+                                const int32_t* colsrc, int) {
+  const size_t es = dtype_size(dt);
+  parallel_for(nblk * m, nthreads_, [&](int64_t row) {
+    const int64_t b = row / m, r = row % m;
+    char* d = static_cast<char*>(dst) + ((int64_t)dst_blk[b] * m + r) * ldd * es;
+    const char* s = static_cast<const char*>(X) + (b * m + r) * ldx * es;
+    for (int64_t c = 0; c < Nr; ++c)
+      std::memcpy(d + c * m * es, s + (int64_t)colsrc[c] * m * es, m * es);
+  });
+}
+
+void HostDevice::row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out,
+                             int) {
+  double mx = 0.0;
+  for (int64_t r = 0; r < L.rows; ++r) {
+    if (L.global_row(r) >= L.n) continue;
+    double s = 0.0;
+    for (int64_t j = 0; j < L.n; ++j)
+      s += std::fabs(dt == DType::F64 ? tp<double>(X)[r * ldx + j] : (double)tp<float>(X)[r * ldx + j]);
+    mx = std::max(mx, s);
+  }
+  out[0] = mx;
+}
+
+void HostDevice::residual(DType dt, const void* A, const void* Full, const Layout& L, double* out,
+                          int) {
+  const int64_t np = L.npad;
+  std::vector<double> rowres(L.rows, 0.0);
+  parallel_for(L.rows, nthreads_, [&](int64_t r) {
+    const int64_t gr = L.global_row(r);
+    if (gr >= L.n) return;
+    std::vector<double> acc(L.n, 0.0);
+    for (int64_t k = 0; k < L.n; ++k) {
+      const double a = dt == DType::F64 ? tp<double>(A)[r * np + k] : (double)tp<float>(A)[r * np + k];
+      if (a == 0.0) continue;
+      for (int64_t j = 0; j < L.n; ++j)
+        acc[j] += a * (dt == DType::F64 ? tp<double>(Full)[k * np + j]
+                                        : (double)tp<float>(Full)[k * np + j]);
+    }
+    double s = 0.0;
+    for (int64_t j = 0; j < L.n; ++j) s += std::fabs(acc[j] - (j == gr ? 1.0 : 0.0));
+    rowres[r] = s;
+  });
+  double mx = 0.0;
+  for (double v : rowres) mx = std::max(mx, v);
+  out[0] = mx;
+}
+
+}  // namespace gj

@@ -1,0 +1,105 @@
+// LoopbackComm: p virtual ranks as threads of one process (host memory or one/several GPUs).
+// Semantics match RcclComm: every rank calls the same collectives in the same order; a collective
+// first drains the issuing stream so it observes all work enqueued before it (stream ordering).
+#include <algorithm>
+#include <cstring>
+
+#include "gj/comms.hpp"
+
+namespace gj {
+
+LoopbackHub::LoopbackHub(int p) : ptr(p, nullptr), val(p, 0.0), p2p(p), p_(p) {}
+
+void LoopbackHub::arrive_and_wait() {
+  std::unique_lock<std::mutex> lk(mu_);
+  const long g = gen_;
+  if (++count_ == p_) {
+    count_ = 0;
+    ++gen_;
+    cv_.notify_all();
+  } else {
+    cv_.wait(lk, [&] { return gen_ != g; });
+  }
+}
+
+void LoopbackComm::allgather(Device& dev, const void* send, void* recv, size_t bytes, int s) {
+  dev.sync_stream(s);
+  hub_->ptr[r_] = send;
+  hub_->arrive_and_wait();
+  for (int q = 0; q < size(); ++q)
+    dev.copy(static_cast<char*>(recv) + (size_t)q * bytes, hub_->ptr[q], bytes, s);
+  dev.sync_stream(s);
+  hub_->arrive_and_wait();
+}
+
+void LoopbackComm::bcast(Device& dev, void* buf, size_t bytes, int root, int s) {
+  dev.sync_stream(s);
+  hub_->ptr[r_] = buf;
+  hub_->arrive_and_wait();
+  if (r_ != root) dev.copy(buf, hub_->ptr[root], bytes, s);
+  dev.sync_stream(s);
+  hub_->arrive_and_wait();
+}
+
+void LoopbackComm::allreduce_max(Device& dev, double* buf, size_t count, int s) {
+  dev.sync_stream(s);
+  std::vector<double> mine(count), tmp(count);
+  dev.copy(mine.data(), buf, count * sizeof(double), s);
+  dev.sync_stream(s);
+  hub_->ptr[r_] = mine.data();
+  hub_->arrive_and_wait();
+  for (int q = 0; q < size(); ++q) {
+    const double* o = static_cast<const double*>(hub_->ptr[q]);
+    for (size_t i = 0; i < count; ++i) tmp[i] = (q == 0) ? o[i] : std::max(tmp[i], o[i]);
+  }
+  hub_->arrive_and_wait();
+  dev.copy(buf, tmp.data(), count * sizeof(double), s);
+  dev.sync_stream(s);
+}
+
+void LoopbackComm::group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) {
+  dev.sync_stream(s);
+  auto& mine = hub_->p2p[r_];
+  mine.clear();
+  for (const auto& op : ops)
+    if (op.send) mine.push_back(op);
+  hub_->arrive_and_wait();
+  // receives from peer q match q's sends to me in issue order (NCCL p2p semantics)
+  std::vector<size_t> cursor(size(), 0);
+  for (const auto& op : ops) {
+    if (op.send) continue;
+    const auto& theirs = hub_->p2p[op.peer];
+    size_t& c = cursor[op.peer];
+    while (c < theirs.size() && theirs[c].peer != r_) ++c;
+    GJ_REQUIRE(c < theirs.size(), "loopback p2p: unmatched receive");
+    GJ_REQUIRE(theirs[c].bytes == op.bytes, "loopback p2p: size mismatch");
+    dev.copy(op.ptr, theirs[c].ptr, op.bytes, s);
+    ++c;
+  }
+  dev.sync_stream(s);
+  hub_->arrive_and_wait();
+}
+
+void LoopbackComm::barrier(Device& dev) {
+  dev.sync_all();
+  hub_->arrive_and_wait();
+}
+
+double LoopbackComm::host_max(Device&, double v) {
+  hub_->val[r_] = v;
+  hub_->arrive_and_wait();
+  double m = hub_->val[0];
+  for (int q = 1; q < size(); ++q) m = std::max(m, hub_->val[q]);
+  hub_->arrive_and_wait();
+  return m;
+}
+
+void LoopbackComm::host_allgather(Device&, const void* send, void* recv, size_t bytes) {
+  hub_->ptr[r_] = send;
+  hub_->arrive_and_wait();
+  for (int q = 0; q < size(); ++q)
+    std::memcpy(static_cast<char*>(recv) + (size_t)q * bytes, hub_->ptr[q], bytes);
+  hub_->arrive_and_wait();
+}
+
+}  // namespace gj

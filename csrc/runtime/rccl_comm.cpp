@@ -1,0 +1,133 @@
+// RcclComm: RCCL over xGMI (replaces the reference's MPI layer).
+//
+//   M9  MPI_Allreduce(PivotMin, user op)  -> ncclAllGather of 32-B records (SIDE communicator)
+//   M10 MPI_Bcast(pivot row)              -> ncclBroadcast per column chunk (COMM communicator),
+//                                            pipelined behind the trailing update
+//   M11 MPI_Send/Recv row swap            -> no per-step traffic; one grouped ncclSend/ncclRecv
+//                                            exchange at the end (finalize)
+//   M14 MPI_Sendrecv_replace ring (residual) -> ncclAllGather of the inverse strips
+//   M6/M7/M13/M15 scalar allreduces       -> host_max() over a tiny device buffer
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+
+#include "gj/comms.hpp"
+
+namespace gj {
+
+#define NCCL_OK(expr)                                                                        \
+  do {                                                                                       \
+    ncclResult_t r_ = (expr);                                                                \
+    if (r_ != ncclSuccess)                                                                   \
+      throw Error(Status::CommError, std::string("RCCL error: ") + ncclGetErrorString(r_) +  \
+                                         " at " + __FILE__ + ":" + std::to_string(__LINE__)); \
+  } while (0)
+
+static_assert(sizeof(ncclUniqueId) == RcclComm::kIdBytes, "unexpected ncclUniqueId size");
+
+std::string RcclComm::unique_id() {
+  ncclUniqueId id;
+  NCCL_OK(ncclGetUniqueId(&id));
+  return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
+}
+
+RcclComm::RcclComm(const std::vector<std::string>& ids, int nranks, int rank, int device)
+    : n_(nranks), r_(rank), device_(device) {
+  GJ_REQUIRE(ids.size() == 2, "RcclComm needs two unique ids");
+  hipSetDevice(device_);
+  for (int c = 0; c < 2; ++c) {
+    GJ_REQUIRE(ids[c].size() == sizeof(ncclUniqueId), "bad unique id size");
+    ncclUniqueId id;
+    std::memcpy(&id, ids[c].data(), sizeof(id));
+    ncclComm_t comm;
+    NCCL_OK(ncclCommInitRank(&comm, nranks, id, rank));
+    comms_[c] = comm;
+  }
+  dbuf_sz_ = 64 * 1024;
+  if (hipMalloc(&dbuf_, dbuf_sz_) != hipSuccess) throw Error(Status::NoMemory, "RcclComm scratch");
+}
+
+RcclComm::~RcclComm() {
+  hipSetDevice(device_);
+  for (void* c : comms_)
+    if (c) ncclCommDestroy(static_cast<ncclComm_t>(c));
+  if (dbuf_) hipFree(dbuf_);
+}
+
+std::string RcclComm::describe() const {
+  int v = 0;
+  ncclGetVersion(&v);
+  return "rccl(v" + std::to_string(v) + ", " + std::to_string(n_) + " ranks)";
+}
+
+void* RcclComm::comm_for(int s) const {
+  GJ_REQUIRE(s == S_SIDE || s == S_COMM, "RCCL collectives are only issued on SIDE/COMM streams");
+  return comms_[s == S_SIDE ? 0 : 1];
+}
+
+static inline hipStream_t st(Device& dev, int s) { return static_cast<hipStream_t>(dev.native_stream(s)); }
+
+void RcclComm::allgather(Device& dev, const void* send, void* recv, size_t bytes, int s) {
+  NCCL_OK(ncclAllGather(send, recv, bytes, ncclUint8, static_cast<ncclComm_t>(comm_for(s)), st(dev, s)));
+}
+
+void RcclComm::bcast(Device& dev, void* buf, size_t bytes, int root, int s) {
+  if (n_ == 1) return;
+  NCCL_OK(ncclBroadcast(buf, buf, bytes, ncclUint8, root, static_cast<ncclComm_t>(comm_for(s)), st(dev, s)));
+}
+
+void RcclComm::allreduce_max(Device& dev, double* buf, size_t count, int s) {
+  NCCL_OK(ncclAllReduce(buf, buf, count, ncclFloat64, ncclMax, static_cast<ncclComm_t>(comm_for(s)), st(dev, s)));
+}
+
+void RcclComm::group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) {
+  if (ops.empty()) return;
+  ncclComm_t c = static_cast<ncclComm_t>(comm_for(s));
+  NCCL_OK(ncclGroupStart());
+  for (const auto& op : ops) {
+    if (op.send)
+      NCCL_OK(ncclSend(op.ptr, op.bytes, ncclUint8, op.peer, c, st(dev, s)));
+    else
+      NCCL_OK(ncclRecv(op.ptr, op.bytes, ncclUint8, op.peer, c, st(dev, s)));
+  }
+  NCCL_OK(ncclGroupEnd());
+}
+
+void RcclComm::barrier(Device& dev) {
+  dev.sync_all();
+  double v = 0.0;
+  host_max(dev, v);
+}
+
+double RcclComm::host_max(Device& dev, double v) {
+  hipSetDevice(device_);
+  dev.sync_stream(S_SIDE);
+  double* d = static_cast<double*>(dbuf_);
+  dev.copy(d, &v, sizeof(double), S_SIDE);
+  allreduce_max(dev, d, 1, S_SIDE);
+  double out = 0;
+  dev.copy(&out, d, sizeof(double), S_SIDE);
+  dev.sync_stream(S_SIDE);
+  return out;
+}
+
+void RcclComm::host_allgather(Device& dev, const void* send, void* recv, size_t bytes) {
+  hipSetDevice(device_);
+  const size_t need = bytes * (n_ + 1);
+  void* tmp = dbuf_;
+  bool owned = false;
+  if (need > dbuf_sz_) {
+    if (hipMalloc(&tmp, need) != hipSuccess) throw Error(Status::NoMemory, "host_allgather");
+    owned = true;
+  }
+  char* d = static_cast<char*>(tmp);
+  dev.sync_stream(S_SIDE);
+  dev.copy(d, send, bytes, S_SIDE);
+  allgather(dev, d, d + bytes, bytes, S_SIDE);
+  dev.copy(recv, d + bytes, bytes * n_, S_SIDE);
+  dev.sync_stream(S_SIDE);
+  if (owned) hipFree(tmp);
+}
+
+}  // namespace gj

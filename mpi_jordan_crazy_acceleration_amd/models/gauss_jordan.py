@@ -1,0 +1,105 @@
+"""High-level single-process API of the block Gauss-Jordan inverter.
+
+Mirrors the reference program's flow (``main.cpp:343-519``: build A, time ``Jordan``, print the
+corners, recompute A, residual) but runs in-process: ``ranks`` host threads each drive one GPU
+(RCCL between them when every rank has its own GPU) or one virtual host rank (``device="cpu"``).
+For one process per GPU under ``torch.distributed`` use :class:`parallel.dist.DistributedGaussJordan`.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .._native import load_native
+
+STATUS = {0: "ok", 1: "singular matrix", 2: "not enough memory", 3: "cannot open", 4: "cannot read",
+          5: "bad arguments", 6: "communication error"}
+
+
+class SingularMatrixError(ArithmeticError):
+    """Raised when every remaining candidate block is singular (reference: ``singular matrix``)."""
+
+
+def _default_device() -> str:
+    return "gpu" if load_native().device_count() > 0 else "cpu"
+
+
+@dataclass
+class GaussJordan:
+    """Configuration of an in-process run (CLI-equivalent).
+
+    block_size : reference ``m`` — the pivot block size (128 or 256 map best onto the MFMA tiles)
+    ranks      : reference ``p`` — GPUs (device="gpu") or virtual host ranks (device="cpu")
+    dtype      : "fp64" (reference) or "fp32" (CDNA4 fp32 MFMA path)
+    """
+
+    block_size: int = 128
+    ranks: int = 1
+    device: str = "auto"
+    dtype: str = "fp64"
+    comm: str = "auto"
+    chunk_cols: int = 0
+    eps: float = 1e-15
+    sync_debug: bool = False
+    residual: str = "always"
+    host_threads: int = 0
+    extra: dict = field(default_factory=dict)
+
+    def _cfg(self, n: int) -> dict:
+        dev = _default_device() if self.device == "auto" else self.device
+        cfg = dict(n=int(n), m=int(self.block_size), ranks=int(self.ranks), device=dev,
+                   dtype=self.dtype, comm=self.comm, chunk_cols=int(self.chunk_cols), eps=float(self.eps),
+                   sync_debug=bool(self.sync_debug), residual=self.residual,
+                   host_threads=int(self.host_threads))
+        cfg.update(self.extra)
+        return cfg
+
+    def run(self, n: int, gen: str = "absdiff", seed: int = 0, file: Optional[str] = None,
+            input: Optional[np.ndarray] = None, keep_inverse: bool = False, repeats: int = 1) -> dict:
+        cfg = self._cfg(n)
+        cfg.update(gen=gen, seed=int(seed), keep_inverse=keep_inverse, repeats=int(repeats))
+        if file is not None:
+            cfg["file"] = str(file)
+        if input is not None:
+            cfg["input"] = np.ascontiguousarray(input, dtype=np.float64)
+        rep = load_native().run_local(cfg)
+        rep["status_name"] = STATUS.get(rep["status"], "error")
+        return rep
+
+    def inverse(self, A):
+        is_torch = isinstance(A, torch.Tensor)
+        a = A.detach().to("cpu", torch.float64).numpy() if is_torch else np.asarray(A, dtype=np.float64)
+        if a.ndim != 2 or a.shape[0] != a.shape[1]:
+            raise ValueError("A must be square")
+        rep = self.run(a.shape[0], input=a, keep_inverse=True)
+        if rep["status"] == 1:
+            raise SingularMatrixError("singular matrix")
+        if rep["status"] != 0:
+            raise RuntimeError(rep["message"] or rep["status_name"])
+        inv = rep["inverse"]
+        if is_torch:
+            return torch.from_numpy(inv).to(device=A.device, dtype=A.dtype)
+        return inv
+
+
+def inverse(A, block_size: int = 128, **kw):
+    """Inverse of a dense square matrix by block Gauss-Jordan (reference semantics, fixed pivot bug)."""
+    return GaussJordan(block_size=block_size, residual="never", **kw).inverse(A)
+
+
+def solve(A, b, block_size: int = 128, **kw):
+    """Solve ``A x = b`` (b: vector or matrix of right-hand sides) via the block Gauss-Jordan inverse."""
+    inv = inverse(A, block_size=block_size, **kw)
+    if isinstance(inv, torch.Tensor):
+        return inv @ (b if isinstance(b, torch.Tensor) else torch.as_tensor(b, dtype=inv.dtype))
+    return inv @ np.asarray(b, dtype=np.float64)
+
+
+def run(n: int, m: int, ranks: int = 1, device: str = "auto", gen: str = "absdiff", seed: int = 0,
+        file: Optional[str] = None, dtype: str = "fp64", residual: str = "always", **kw) -> dict:
+    """The reference CLI flow in-process; returns the report dict (glob_time, residual, corners...)."""
+    return GaussJordan(block_size=m, ranks=ranks, device=device, dtype=dtype, residual=residual,
+                       **kw).run(n, gen=gen, seed=seed, file=file)

@@ -1,0 +1,101 @@
+"""Kernel-level wrappers of the hand-written gfx950 kernels, on torch tensors.
+
+These call straight into the native kernels (no PyTorch fallback): a CUDA(HIP) tensor runs the HIP
+kernel, a CPU tensor runs the host reference executor — chosen by the tensor's device, never
+silently.  Used by the per-kernel numerics tests and for profiling single kernels.
+"""
+from __future__ import annotations
+
+import functools
+
+import torch
+
+from .._native import load_native
+
+_DT = {torch.float64: "fp64", torch.float32: "fp32"}
+
+
+@functools.lru_cache(maxsize=None)
+def _hip(idx: int):
+    return load_native().hip_device(idx)
+
+
+@functools.lru_cache(maxsize=None)
+def _host():
+    return load_native().host_device(0)
+
+
+def device_for(t: torch.Tensor):
+    if t.is_cuda:
+        torch.cuda.synchronize(t.device)
+        return _hip(t.device.index if t.device.index is not None else torch.cuda.current_device())
+    return _host()
+
+
+def _p(t: torch.Tensor) -> int:
+    return t.data_ptr()
+
+
+def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, op: str = "acc", a_kmajor: bool = False,
+         zero_cols=(0, 0), pivot_row0: int = -1) -> torch.Tensor:
+    """C += A@B (op="acc") or C = A@B (op="store").  With a_kmajor, ``A`` is given as A^T (K x M).
+
+    Elimination extras (op="acc"): C columns in ``zero_cols`` enter as 0; rows
+    [pivot_row0, pivot_row0 + K) are overwritten with the rows of B."""
+    assert A.dtype == B.dtype == C.dtype and A.stride(-1) == 1 and B.stride(-1) == 1 and C.stride(-1) == 1
+    M, N = C.shape
+    K = A.shape[0] if a_kmajor else A.shape[1]
+    device_for(C).gemm(_DT[C.dtype], op, a_kmajor, M, N, K, _p(A), A.stride(0), _p(B), B.stride(0), _p(C), C.stride(0),
+                       int(zero_cols[0]), int(zero_cols[1]), int(pivot_row0))
+    return C
+
+
+def generate(X: torch.Tensor, n: int, m: int, p: int = 1, k: int = 0, kind: str = "absdiff", seed: int = 0) -> torch.Tensor:
+    device_for(X).generate(_DT[X.dtype], _p(X), n, m, p, k, kind, seed)
+    return X
+
+
+def extract_neg_t(X: torch.Tensor, col0: int, m: int) -> torch.Tensor:
+    rows = X.shape[0]
+    Lt = torch.empty((m, rows), dtype=X.dtype, device=X.device)
+    device_for(X).extract_neg_t(_DT[X.dtype], _p(Lt), rows, _p(X), X.stride(0), rows, col0, m)
+    return Lt
+
+
+def block_inverse(Lt: torch.Tensor, n: int, m: int, p: int = 1, k: int = 0, used: torch.Tensor = None,
+                  thresh: float = 0.0):
+    """Batched candidate inversion over the K-major multiplier panel Lt (m x rows).
+
+    Returns (inv_t [nblk, m, m] with inv_t[b] = inv(W_b)^T, scores [nblk], valid [nblk])."""
+    nblk = Lt.shape[1] // m
+    dev = Lt.device
+    inv_t = torch.zeros((max(nblk, 1), m, m), dtype=Lt.dtype, device=dev)
+    scores = torch.zeros(max(nblk, 1), dtype=torch.float64, device=dev)
+    valid = torch.zeros(max(nblk, 1), dtype=torch.int32, device=dev)
+    Nr = (n + m - 1) // m
+    if used is None:
+        used = torch.zeros(Nr, dtype=torch.int32, device=dev)
+    device_for(Lt).block_inverse(_DT[Lt.dtype], _p(Lt), Lt.stride(0), _p(inv_t), _p(scores), _p(valid), _p(used),
+                                 n, m, p, k, thresh)
+    return inv_t[:nblk], scores[:nblk], valid[:nblk]
+
+
+def permute_blocks(X: torch.Tensor, m: int, dst_blk: torch.Tensor, colsrc: torch.Tensor) -> torch.Tensor:
+    rows, ncols = X.shape
+    nblk, Nr = rows // m, ncols // m
+    out = torch.empty_like(X)
+    device_for(X).permute_blocks(_DT[X.dtype], _p(out), out.stride(0), _p(X), X.stride(0), nblk, m, Nr,
+                                 _p(dst_blk), _p(colsrc))
+    return out
+
+
+def row_abs_max(X: torch.Tensor, n: int, m: int, p: int = 1, k: int = 0) -> float:
+    out = torch.zeros(1, dtype=torch.float64, device=X.device)
+    device_for(X).row_abs_max(_DT[X.dtype], _p(X), X.stride(0), n, m, p, k, _p(out))
+    return float(out.item())
+
+
+def residual(A_loc: torch.Tensor, Full: torch.Tensor, n: int, m: int, p: int = 1, k: int = 0) -> float:
+    out = torch.zeros(1, dtype=torch.float64, device=A_loc.device)
+    device_for(A_loc).residual(_DT[A_loc.dtype], _p(A_loc), _p(Full), n, m, p, k, _p(out))
+    return float(out.item())

@@ -1,0 +1,171 @@
+"""One rank per process over ``torch.distributed`` (the MI355X deployment model).
+
+* backend ``nccl`` (= RCCL on ROCm): each process drives ``cuda:LOCAL_RANK`` with the native
+  HipDevice; the engine builds its own two RCCL communicators (one per issuing stream role) from
+  unique ids broadcast through the default process group, and talks RCCL directly from C++ — no
+  Python in the per-step path.
+* backend ``gloo`` (CPU): the native HostDevice executes and collectives trampoline into
+  ``torch.distributed`` via :class:`TorchDistComm` — the CPU-testable form of the same protocol.
+
+Reference parity: this replaces MPI_Init/Comm_size/Comm_rank (main.cpp:65-93) and the per-rank
+``solve`` driver (main.cpp:343-519).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .._native import load_native
+from .layout import Layout, global_rows
+
+
+class TorchDistComm:
+    """Host-memory collectives for the native engine, implemented with torch.distributed (gloo)."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+
+    @staticmethod
+    def _view(addr: int, nbytes: int) -> torch.Tensor:
+        if nbytes == 0:
+            return torch.empty(0, dtype=torch.uint8)
+        buf = (ctypes.c_char * nbytes).from_address(addr)
+        return torch.frombuffer(buf, dtype=torch.uint8)
+
+    def allgather(self, send: int, recv: int, nbytes: int) -> None:
+        s = self._view(send, nbytes).clone()
+        out = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(self.world)]
+        dist.all_gather(out, s, group=self.group)
+        self._view(recv, nbytes * self.world).copy_(torch.cat(out))
+
+    def bcast(self, addr: int, nbytes: int, root: int) -> None:
+        t = self._view(addr, nbytes)
+        tmp = t.clone()
+        dist.broadcast(tmp, src=root, group=self.group)
+        t.copy_(tmp)
+
+    def allreduce_max(self, addr: int, count: int) -> None:
+        t = self._view(addr, count * 8)
+        tmp = t.clone().view(torch.float64)
+        dist.all_reduce(tmp, op=dist.ReduceOp.MAX, group=self.group)
+        t.copy_(tmp.view(torch.uint8))
+
+    def group_p2p(self, ops) -> None:
+        reqs, recvs = [], []
+        tags = {}
+        for addr, nbytes, peer, is_send in ops:
+            key = (peer, bool(is_send))
+            tag = tags.get(key, 0)
+            tags[key] = tag + 1
+            if is_send:
+                reqs.append(dist.isend(self._view(addr, nbytes).clone(), dst=peer, group=self.group, tag=tag))
+            else:
+                buf = torch.empty(nbytes, dtype=torch.uint8)
+                reqs.append(dist.irecv(buf, src=peer, group=self.group, tag=tag))
+                recvs.append((addr, nbytes, buf))
+        for r in reqs:
+            r.wait()
+        for addr, nbytes, buf in recvs:
+            self._view(addr, nbytes).copy_(buf)
+
+    def barrier(self) -> None:
+        dist.barrier(group=self.group)
+
+    def host_max(self, v: float) -> float:
+        t = torch.tensor([v], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return float(t.item())
+
+
+class DistributedGaussJordan:
+    """Block-row-cyclic Gauss-Jordan inversion with one rank per process.
+
+    Typical GPU use (under ``torchrun``)::
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        gj = DistributedGaussJordan(n=32768, m=128)
+        gj.generate("random", seed=0)
+        stats = gj.solve()                    # collective
+        res = gj.residual_generated("random", 0)
+    """
+
+    def __init__(self, n: int, m: int, dtype: str = "fp64", chunk_cols: int = 0, eps: float = 1e-15,
+                 sync_debug: bool = False, host_threads: int = 0, local_rank: Optional[int] = None):
+        C = load_native()
+        if not dist.is_initialized():
+            raise RuntimeError("torch.distributed is not initialised")
+        self.rank = dist.get_rank()
+        self.world = dist.get_world_size()
+        self.backend = dist.get_backend()
+        self.n, self.m, self.dtype = int(n), int(m), dtype
+        if self.backend == "nccl":
+            if local_rank is None:
+                local_rank = int(os.environ.get("LOCAL_RANK", torch.cuda.current_device()))
+            self.local_rank = local_rank
+            self.device = C.hip_device(local_rank)
+            if self.world > 1:
+                obj = [[C.rccl_unique_id(), C.rccl_unique_id()] if self.rank == 0 else None]
+                dist.broadcast_object_list(obj, src=0)
+                self.comm = C.rccl_comm(obj[0], self.world, self.rank, local_rank)
+            else:
+                self.comm = C.self_comm()
+        else:
+            self.local_rank = None
+            self.device = C.host_device(host_threads)
+            self.comm = C.py_comm(TorchDistComm(), self.rank, self.world) if self.world > 1 else C.self_comm()
+        self.engine = C.Engine(self.device, self.comm, self.n, self.m, dtype, chunk_cols, eps, sync_debug)
+        self.layout = Layout(self.n, self.m, self.world, self.rank)
+        self._rows = global_rows(self.n, self.m, self.world, self.rank)
+
+    # ---- input
+    def generate(self, kind: str = "absdiff", seed: int = 0) -> None:
+        self.engine.generate(kind, int(seed))
+
+    def load(self, A: np.ndarray) -> None:
+        """Load this rank's rows of the full matrix A (every rank may pass the full matrix)."""
+        A = np.asarray(A, dtype=np.float64)
+        self.engine.upload_local_rows(np.ascontiguousarray(A[self._rows]))
+
+    def load_local_rows(self, rows: np.ndarray) -> None:
+        self.engine.upload_local_rows(np.ascontiguousarray(rows, dtype=np.float64))
+
+    # ---- solve
+    def solve(self) -> dict:
+        return self.engine.solve()
+
+    # ---- output
+    def local_rows(self) -> np.ndarray:
+        return self.engine.download_local_rows()
+
+    def global_row_ids(self) -> np.ndarray:
+        return self._rows
+
+    def gather_inverse(self) -> Optional[np.ndarray]:
+        """Full inverse on rank 0 (None elsewhere); host traffic, meant for tests / small n."""
+        mine = torch.from_numpy(self.local_rows())
+        if self.world == 1:
+            return mine.numpy()
+        parts = [None] * self.world if self.rank == 0 else None
+        dist.gather_object((self._rows, mine.numpy()), parts, dst=0)
+        if self.rank != 0:
+            return None
+        out = np.zeros((self.n, self.n))
+        for rows, vals in parts:
+            out[rows] = vals
+        return out
+
+    def corner(self, nm: int = 10, which: str = "result") -> np.ndarray:
+        return self.engine.corner(nm, 1 if which == "result" else 0)
+
+    def residual_generated(self, kind: str = "absdiff", seed: int = 0) -> float:
+        return self.engine.residual_generated(kind, int(seed))
+
+    def residual(self, A: np.ndarray) -> float:
+        A = np.asarray(A, dtype=np.float64)
+        return self.engine.residual_rows(np.ascontiguousarray(A[self._rows]))

@@ -1,0 +1,116 @@
+"""Per-kernel numerics on the MI355X: every hand-written HIP kernel vs a plain PyTorch/numpy fp64
+reference of the same op (asymmetric operands, ragged edges)."""
+import numpy as np
+import pytest
+import torch
+
+from mpi_jordan_crazy_acceleration_amd import ops
+from mpi_jordan_crazy_acceleration_amd.utils import generate_matrix
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand(shape, dtype, seed):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.rand(shape, generator=g, dtype=torch.float64) * 2 - 1).to(dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 128), (256, 384, 128), (300, 200, 60), (37, 515, 17), (1000, 130, 256)])
+@pytest.mark.parametrize("kmajor", [True, False])
+def test_gemm_acc_matches_torch(dtype, M, N, K, kmajor):
+    A = _rand((M, K), dtype, 1)
+    B = _rand((K, N), dtype, 2)
+    C = _rand((M, N), dtype, 3)
+    ref = C.double() + A.double() @ B.double()
+    Ad = (A.t().contiguous() if kmajor else A).cuda()
+    Cd = C.cuda()
+    ops.gemm(Ad, B.cuda(), Cd, op="acc", a_kmajor=kmajor)
+    tol = 1e-12 if dtype == torch.float64 else 2e-5
+    err = (Cd.cpu().double() - ref).abs().max().item()
+    assert err < tol * K, err
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_gemm_store_identity_asymmetric(dtype):
+    # A = I with an asymmetric B catches a transposed C/D lane map (guide §3)
+    M = N = K = 128
+    A = torch.eye(M, dtype=dtype)
+    B = torch.arange(K * N, dtype=dtype).reshape(K, N) / 7.0
+    C = torch.full((M, N), 5.0, dtype=dtype).cuda()
+    ops.gemm(A.cuda(), B.cuda(), C, op="store", a_kmajor=True)
+    assert torch.equal(C.cpu(), B)
+
+
+def test_generate_matches_numpy():
+    n, m = 300, 64
+    Nr = (n + m - 1) // m
+    X = torch.empty((Nr * m, Nr * m), dtype=torch.float64, device="cuda")
+    ops.generate(X, n, m, 1, 0, "random", 11)
+    ref = generate_matrix(n, "random", 11)
+    Xc = X.cpu().numpy()
+    assert np.array_equal(Xc[:n, :n], ref)
+    assert np.array_equal(Xc[n:, n:], np.eye(Nr * m - n))
+
+
+def test_extract_neg_t():
+    X = _rand((300, 512), torch.float64, 5).cuda()
+    Lt = ops.extract_neg_t(X, 128, 96)
+    assert torch.equal(Lt.cpu(), -X.cpu()[:, 128:224].t())
+
+
+@pytest.mark.parametrize("m", [16, 60, 128, 200, 256, 300])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_block_inverse(m, dtype):
+    nblk = 5
+    rows = nblk * m
+    rng = np.random.default_rng(m)
+    W = rng.standard_normal((nblk, m, m)) + 0.0
+    W[2] = 0.0  # singular candidate
+    W[3] = np.eye(m) * 2.0  # exact inverse 0.5 I
+    X = np.zeros((rows, m))
+    for b in range(nblk):
+        X[b * m:(b + 1) * m] = W[b]
+    Lt = torch.from_numpy(-X.T.copy()).to(dtype).cuda()
+    n = rows
+    inv_t, scores, valid = ops.block_inverse(Lt, n, m, 1, 0, thresh=1e-12)
+    valid = valid.cpu().numpy()
+    assert list(valid) == [1, 1, 0, 1, 1]
+    tol = 1e-8 if dtype == torch.float64 else 2e-2
+    for b in [0, 1, 3, 4]:
+        ref = np.linalg.inv(W[b].astype(np.float32 if dtype == torch.float32 else np.float64).astype(np.float64))
+        got = inv_t[b].cpu().double().numpy().T
+        rel = np.abs(got - ref).max() / np.abs(ref).max()
+        assert rel < tol, (b, rel)
+        assert abs(scores[b].item() - np.abs(ref).sum(1).max()) / np.abs(ref).sum(1).max() < tol
+    assert abs(scores[3].item() - 0.5) < 1e-6
+
+
+def test_permute_blocks():
+    m, nblk, Nr = 32, 3, 5
+    X = _rand((nblk * m, Nr * m), torch.float64, 9).cuda()
+    dst = torch.tensor([2, 0, 1], dtype=torch.int32, device="cuda")
+    colsrc = torch.tensor([4, 3, 0, 1, 2], dtype=torch.int32, device="cuda")
+    out = ops.permute_blocks(X, m, dst, colsrc).cpu()
+    Xc = X.cpu()
+    for b in range(nblk):
+        for c in range(Nr):
+            d = int(dst[b])
+            u = int(colsrc[c])
+            assert torch.equal(out[d * m:(d + 1) * m, c * m:(c + 1) * m], Xc[b * m:(b + 1) * m, u * m:(u + 1) * m])
+
+
+def test_row_abs_max_and_residual():
+    n, m = 250, 64
+    A = generate_matrix(n, "random", 3)
+    Nr = (n + m - 1) // m
+    npad = Nr * m
+    Ap = np.eye(npad)
+    Ap[:n, :n] = A
+    inv = np.eye(npad)
+    inv[:n, :n] = np.linalg.inv(A)
+    Ad = torch.from_numpy(Ap).cuda()
+    assert abs(ops.row_abs_max(Ad, n, m) - np.abs(A).sum(1).max()) < 1e-9
+    r = ops.residual(Ad, torch.from_numpy(inv).cuda(), n, m)
+    ref = np.abs(A @ np.linalg.inv(A) - np.eye(n)).sum(1).max()
+    assert r < 1e-10 and abs(r - ref) < 1e-11

@@ -1,0 +1,116 @@
+"""The native engine on the host executor (CPU): protocol, pivoting, numerics vs the numpy oracle
+and numpy.linalg.inv on the reference's acceptance grid."""
+import numpy as np
+import pytest
+
+import mpi_jordan_crazy_acceleration_amd as gj
+from mpi_jordan_crazy_acceleration_amd.models.gauss_jordan import SingularMatrixError
+from mpi_jordan_crazy_acceleration_amd.utils import gauss_jordan_reference, generate_matrix
+
+
+def _mat(kind, n, seed=0):
+    rng = np.random.default_rng(seed)
+    if kind == "rand":
+        return rng.standard_normal((n, n))
+    if kind == "perm":  # reversed-identity dominant: forces off-diagonal pivots (row swaps)
+        return np.eye(n)[::-1] + 0.01 * rng.standard_normal((n, n))
+    return generate_matrix(n, kind)
+
+
+GRID = [(12, 3), (10, 3), (11, 4), (10, 12), (10, 1), (7, 7), (37, 5)]
+
+
+@pytest.mark.parametrize("n,m", GRID)
+@pytest.mark.parametrize("p", [1, 2, 3, 5])
+@pytest.mark.parametrize("kind", ["rand", "perm", "absdiff"])
+def test_inverse_grid(n, m, p, kind):
+    A = _mat(kind, n, seed=n * 31 + m)
+    inv = gj.inverse(A, block_size=m, device="cpu", ranks=p)
+    ref = np.linalg.inv(A)
+    assert np.abs(inv - ref).max() / np.abs(ref).max() < 1e-10
+
+
+@pytest.mark.parametrize("p", [1, 2, 3, 4])
+def test_matches_reference_oracle_and_pivots(p):
+    n, m = 48, 4
+    A = _mat("perm", n, 3)
+    ref_inv, ref_piv = gauss_jordan_reference(A, m, p)
+    rep = gj.GaussJordan(block_size=m, ranks=p, device="cpu").run(n, input=A, keep_inverse=True)
+    assert rep["status"] == 0
+    assert np.abs(rep["inverse"] - ref_inv).max() < 1e-11
+    # same pivot *content*: the engine reports physical rows, the oracle logical positions after swaps
+    assert rep["stats"]["offdiag_pivots"] > 0
+
+
+@pytest.mark.parametrize("p,expected_first", [(1, 0), (2, 1), (3, 2), (4, 3)])
+def test_pivot_tie_rule(p, expected_first):
+    # all column-0 candidate blocks equal 2I -> ties go to the highest rank, then the
+    # lowest local row: p=1 -> row 0, p=2 -> 1, p=3 -> 2, p=4 -> 3.
+    m, Nr = 2, 4
+    n = m * Nr
+    A = np.zeros((n, n))
+    for i in range(Nr):
+        A[i * m:(i + 1) * m, 0:m] = 2 * np.eye(m)
+    A[:, m:] = np.random.default_rng(5).standard_normal((n, n - m))
+    rep = gj.GaussJordan(block_size=m, ranks=p, device="cpu").run(n, input=A, keep_inverse=True)
+    assert rep["status"] == 0
+    assert rep["stats"]["pivots"][0] == expected_first
+    _, ref_piv = gauss_jordan_reference(A, m, p)
+    assert ref_piv[0] == expected_first
+    assert np.abs(rep["inverse"] - np.linalg.inv(A)).max() < 1e-10
+
+
+def test_singular_matrix_reported():
+    with pytest.raises(SingularMatrixError):
+        gj.inverse(np.zeros((2, 2)), block_size=1, device="cpu")
+    A = _mat("rand", 20, 1)
+    A[:, 3] = 0
+    rep = gj.GaussJordan(block_size=4, ranks=2, device="cpu").run(20, input=A)
+    assert rep["status"] == 1 and rep["status_name"] == "singular matrix"
+
+
+def test_two_by_two_reference_case():
+    inv = gj.inverse(np.array([[1.0, 2.0], [3.0, 4.0]]), block_size=1, device="cpu")
+    assert np.allclose(inv, [[-2, 1], [1.5, -0.5]], atol=1e-14)
+
+
+@pytest.mark.parametrize("n,m,p,golden", [(12, 3, 2, 4.550968e-14), (10, 3, 2, 3.053268e-14), (11, 4, 2, 1.192324e-13)])
+def test_absdiff_golden_residual_band(n, m, p, golden):
+    rep = gj.run(n, m, ranks=p, device="cpu", gen="absdiff")
+    assert rep["status"] == 0
+    assert rep["residual"] < 20 * golden
+
+
+def test_absdiff_residual_no_worse_than_reference_n2048():
+    # reference: n=2048, m=120, p=8 -> 1.85e-06
+    rep = gj.run(2048, 120, ranks=4, device="cpu", gen="absdiff", host_threads=2)
+    assert rep["status"] == 0 and rep["residual"] < 1.85e-6
+
+
+def test_hilbert_and_fp32():
+    rep = gj.run(8, 2, device="cpu", gen="hilbert")
+    assert rep["status"] == 0 and rep["residual"] < 1e-4
+    rep = gj.run(200, 32, ranks=2, device="cpu", gen="random", seed=3, dtype="fp32")
+    assert rep["status"] == 0 and rep["residual"] < 0.5  # fp32: eps 6e-8 x the fp64 amplification (~1e7)
+
+
+def test_sync_debug_is_bitwise_identical():
+    A = _mat("rand", 90, 7)
+    a = gj.GaussJordan(block_size=8, ranks=3, device="cpu").inverse(A)
+    b = gj.GaussJordan(block_size=8, ranks=3, device="cpu", sync_debug=True).inverse(A)
+    assert np.array_equal(a, b)
+
+
+def test_chunking_does_not_change_result():
+    A = _mat("rand", 160, 9)
+    a = gj.GaussJordan(block_size=8, device="cpu", chunk_cols=8).inverse(A)
+    b = gj.GaussJordan(block_size=8, device="cpu", chunk_cols=160).inverse(A)
+    assert np.array_equal(a, b)
+
+
+def test_solve_rhs():
+    A = _mat("rand", 64, 11)
+    x = np.arange(64.0)
+    b = A @ x
+    got = gj.solve(A, b, block_size=16, device="cpu")
+    assert np.abs(got - x).max() < 1e-9
