@@ -31,13 +31,15 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=32768)
-    ap.add_argument("--m", type=int, default=128, help="pivot block size")
+    ap.add_argument("--size", dest="n", type=int, default=32768, help="matrix order N")
+    ap.add_argument("--block", dest="m", type=int, default=128, help="pivot block size m")
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
     ap.add_argument("--gen", default="random")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--chunk-cols", type=int, default=0)
     ap.add_argument("--no-residual", action="store_true")
+    ap.add_argument("--force-rccl", action="store_true", help="use the RCCL communicator even at 1 rank")
+    ap.add_argument("--gemm-variant", default=None, help="big | narrow | tall (kernel tile config)")
     args = ap.parse_args()
 
     import torch
@@ -54,8 +56,13 @@ def main() -> int:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         return 2
     torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if args.gemm_variant:
+        C.set_gemm_variant(args.gemm_variant)
+    if world > 1 or args.force_rccl:
+        if not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world)
         ids = [[C.rccl_unique_id(), C.rccl_unique_id()] if rank == 0 else None]
         dist.broadcast_object_list(ids, src=0)
         dev = C.hip_device(local)
@@ -66,7 +73,7 @@ def main() -> int:
     eng = C.Engine(dev, comm, args.n, args.m, args.dtype, args.chunk_cols)
 
     def barrier():
-        if world > 1:
+        if dist.is_initialized():
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -88,7 +95,7 @@ def main() -> int:
     barrier()
     t1 = time.perf_counter()
     ms = (t1 - t0) * 1e3 / max(args.steps, 1)
-    if world > 1:
+    if dist.is_initialized():
         t = torch.tensor([ms, max(inner)], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ms, inner_max = float(t[0]), float(t[1])
@@ -128,7 +135,7 @@ def main() -> int:
             "host_wait_ms": round(st["host_wait_ms"], 3),
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
     return 0
 

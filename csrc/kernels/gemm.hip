@@ -2,31 +2,59 @@
 //
 //   MODE_ACC   : C[M x N] += A * B       (the elimination update, reference mult_substr_block
 //                                          main.cpp:151-206 called from the hot loop :1165-1194)
+//                with two fused extras: C columns [zc0, zc1) enter as 0 (pivot block column,
+//                X[i,t] := -L_i H) and rows [pr0, pr0 + K) are written with B (the pivot row R_t)
 //   MODE_STORE : C[M x N]  = A * B       (pivot-row normalisation, reference mult_block
 //                                          main.cpp:888-950 called at :1136-1159)
 //   MODE_RESID : per-row partial sums of |A*B - I| (residual, reference matrix_mult_matrix +
 //                                          minus_i + norm, main.cpp:534-667, fused: no D matrix)
 //
-// Tiling (CDNA4, wave64): 128 x 128 output tile per 256-thread workgroup, 4 waves in a 2 x 2 grid,
-// each wave owns 64 x 64 = 4 x 4 MFMA tiles of 16 x 16.  fp64 uses v_mfma_f64_16x16x4_f64 (C/D map
-// col = lane&15, row = (lane>>4) + 4*reg), fp32 uses v_mfma_f32_16x16x4_f32 (row = 4*(lane>>4) + reg).
-// The accumulator is initialised straight from C in the MFMA C/D layout (MODE_ACC), so the
-// read-modify-write needs no separate epilogue pass.  K is staged through LDS in BK = 16 slices,
-// double-buffered (one barrier per slice); both operands are stored K-major in LDS with a 16-element
-// pad so the fragment reads (lanes 0-15 / 16-31 on consecutive k rows) are bank-conflict free.
-// Launch bounds allow 2 workgroups per CU (73.7 KiB LDS each) so one workgroup's C load/store
-// overlaps the other's MFMA stream.
+// Tiling (CDNA4, wave64): 128 x 128 output tile per 512-thread workgroup, 8 waves in a 2 x 4 grid,
+// each wave owns 64 x 32 = 4 x 2 MFMA tiles of 16 x 16 (64 accumulator VGPRs for fp64), so two
+// workgroups (4 waves per SIMD) fit in 128 VGPRs and hide each other's C load/store latency.
+// fp64 uses v_mfma_f64_16x16x4_f64 (C/D map col = lane&15, row = (lane>>4) + 4*reg), fp32 uses
+// v_mfma_f32_16x16x4_f32 (row = 4*(lane>>4) + reg).  The accumulator is initialised straight from C
+// in the MFMA C/D layout, so the read-modify-write needs no separate epilogue pass.
+// K is staged through LDS in BK = 16 slices, double-buffered (one barrier per slice); both operands
+// are K-major in LDS with a 16-element pad so the fragment reads (lanes 0-15 / 16-31 on consecutive
+// k rows) are bank-conflict free.  All global traffic uses buffer loads/stores on a per-tile (or
+// per-slice) resource with one shared 32-bit per-lane offset plus SGPR/immediate offsets: that is
+// what keeps the 32 C addresses per lane out of the register file (no spills at 128 VGPRs).
+// f64 MFMA issue is slow (64 cycles per 16x16x4), so LDS bandwidth is a non-issue: 6 ds_read_b64
+// feed 8 MFMAs (512 cycles) per k4 step.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
+#include <string>
 
 #include "kernels.hpp"
 
 namespace gj {
 namespace kern {
 
-constexpr int BM = 128, BN = 128, BK = 16, NT = 256, PADL = 16;
-constexpr int LDSR = BM + PADL;  // LDS row length (elements) of a K-major slice
+constexpr int PADL = 16;                          // LDS row pad (elements): conflict-free frag reads
+constexpr int kRecords = 0x7ffffff0;              // buffer extent; every access is masked explicitly
+
+// Tile configurations.  WM x WN waves, each owning a (BM/WM) x (BN/WN) block of 16x16 MFMA tiles.
+// OCC = workgroups per CU the launch bounds are written for.
+template <int BM_, int BN_, int BK_, int WM_, int WN_, int OCC_>
+struct Cfg {
+  static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_, WN = WN_, OCC = OCC_;
+  static constexpr int NT = 64 * WM * WN;
+  static constexpr int TM = BM / WM, TN = BN / WN;
+  static constexpr int MI = TM / 16, NJ = TN / 16;
+  static constexpr int SPA = BK * BM / NT, SPB = BK * BN / NT;  // staged elements per thread
+  static constexpr int LDA = BM + PADL, LDB = BN + PADL;         // LDS row lengths
+  static constexpr int WAVES_PER_SIMD = OCC * WM * WN / 4;
+  static_assert(NT % BM == 0 && NT % BN == 0, "thread count must tile the slice rows");
+  static_assert(SPA >= 1 && SPB >= 1 && MI >= 1 && NJ >= 1, "bad tile config");
+};
+using CfgBig = Cfg<128, 128, 16, 2, 4, 2>;   // 512 threads, 2 WG/CU (73.7 KiB LDS each)
+using CfgNarrow = Cfg<128, 64, 8, 2, 2, 4>;  // 256 threads, 4 WG/CU (28.7 KiB LDS each)
+using CfgTall = Cfg<64, 128, 8, 1, 4, 4>;    // 256 threads, 4 WG/CU
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 template <typename T>
 struct Mfma;
@@ -37,7 +65,9 @@ struct Mfma<double> {
   static __device__ __forceinline__ acc_t op(double a, double b, acc_t c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
   }
-  static __device__ __forceinline__ int row_of(int lane, int q) { return (lane >> 4) + 4 * q; }
+  // row_of(lane, q) = rl(lane) + rq(q)
+  static __device__ __forceinline__ int rl(int lane) { return lane >> 4; }
+  static constexpr int rq(int q) { return 4 * q; }
 };
 
 template <>
@@ -46,8 +76,31 @@ struct Mfma<float> {
   static __device__ __forceinline__ acc_t op(float a, float b, acc_t c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
   }
-  static __device__ __forceinline__ int row_of(int lane, int q) { return 4 * (lane >> 4) + q; }
+  static __device__ __forceinline__ int rl(int lane) { return 4 * (lane >> 4); }
+  static constexpr int rq(int q) { return q; }
 };
+
+// ---- buffer load/store of one element (32-bit lane offset + SGPR offset, both in bytes)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, kRecords, 0x00020000);
+}
+template <typename T>
+__device__ __forceinline__ T bload(__amdgpu_buffer_rsrc_t r, int voff, int soff);
+template <>
+__device__ __forceinline__ double bload<double>(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+  return __builtin_bit_cast(double, v);
+}
+template <>
+__device__ __forceinline__ float bload<float>(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+__device__ __forceinline__ void bstore(double v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, voff, soff, 0);
+}
+__device__ __forceinline__ void bstore(float v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, voff, soff, 0);
+}
 
 enum { MODE_ACC = 0, MODE_STORE = 1, MODE_RESID = 2 };
 
@@ -76,11 +129,15 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
 }
 
-template <typename T, int AL, int MODE>
-__global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
+template <typename T, int AL, int MODE, typename CF>
+__global__ __launch_bounds__(CF::NT, CF::WAVES_PER_SIMD) void gemm_kernel(GemmArgs g) {
   using MF = Mfma<T>;
   using acc_t = typename MF::acc_t;
-  __shared__ T lds[2][2][BK][LDSR];  // [buf][A/B][k][row or col]
+  constexpr int ES = sizeof(T);
+  constexpr int BM = CF::BM, BN = CF::BN, BK = CF::BK, WN = CF::WN, NT = CF::NT;
+  constexpr int TM = CF::TM, TN = CF::TN, MI = CF::MI, NJ = CF::NJ;
+  __shared__ T ldsA[2][BK][CF::LDA];  // K-major A slices (double-buffered)
+  __shared__ T ldsB[2][BK][CF::LDB];  // B slices
 
   const int nwg = g.tiles_m * g.tiles_n;
   const int tile = xcd_remap((int)blockIdx.x, nwg);
@@ -89,64 +146,94 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  const T* __restrict__ A = static_cast<const T*>(g.A);
-  const T* __restrict__ B = static_cast<const T*>(g.B);
-  T* __restrict__ C = static_cast<T*>(g.C);
+  const int wm = wid / WN, wn = wid % WN;
+  const T* A = static_cast<const T*>(g.A);
+  const T* B = static_cast<const T*>(g.B);
+  T* C = static_cast<T*>(g.C);
+  const int ldc = (int)g.ldc, ldb = (int)g.ldb, lda = (int)g.lda;
 
-  acc_t acc[4][4];
+  // C addressing: tile resource, one per-lane offset, (i, q) row offsets in SGPRs, j as immediate
+  const int rlane = wm * TM + MF::rl(lane);  // row within the tile (minus i*16 + rq)
+  const int clane = wn * TN + (lane & 15);   // col within the tile (minus j*16)
+  // all masks in 32-bit tile-relative form (row/col bounds and the pivot rows/zero columns)
+  const int Mt = (int)((g.M - m0) < BM ? (g.M - m0) : BM);
+  const int Nt = (int)((g.N - n0) < BN ? (g.N - n0) : BN);
+  const int64_t zlo = g.zc0 - n0, zhi = g.zc1 - n0;
+  const int z0 = (int)(zlo < 0 ? 0 : (zlo > BN ? BN : zlo)), z1 = (int)(zhi < 0 ? 0 : (zhi > BN ? BN : zhi));
+  const int64_t plo = g.pr0 - m0, phi = g.pr0 + g.K - m0;
+  const int p0 = (int)(plo < 0 ? 0 : (plo > BM ? BM : plo)), p1 = (int)(phi < 0 ? 0 : (phi > BM ? BM : phi));
+  __amdgpu_buffer_rsrc_t rc = rsrc(MODE == MODE_RESID ? (const void*)A : (const void*)(C + m0 * g.ldc + n0));
+  const int cvoff = (rlane * ldc + clane) * ES;
+
+  acc_t acc[MI][NJ];
   if (MODE == MODE_ACC) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t col = n0 + wn * 64 + j * 16 + (lane & 15);
+      for (int q = 0; q < 4; ++q) {
+        const int r = rlane + i * 16 + MF::rq(q);
+        const int soff = (i * 16 + MF::rq(q)) * ldc * ES;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int64_t row = m0 + wm * 64 + i * 16 + MF::row_of(lane, q);
-          const bool zero = (col >= g.zc0 && col < g.zc1);
-          acc[i][j][q] = (row < g.M && col < g.N && !zero) ? C[row * g.ldc + col] : T(0);
+        for (int j = 0; j < NJ; ++j) {
+          const int c = clane + j * 16;
+          const bool ok = r < Mt && c < Nt && !(c >= z0 && c < z1);
+          acc[i][j][q] = ok ? bload<T>(rc, cvoff + j * 16 * ES, soff) : T(0);
         }
       }
   } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = acc_t{0, 0, 0, 0};
+      for (int j = 0; j < NJ; ++j) acc[i][j] = acc_t{0, 0, 0, 0};
   }
 
-  // ---- global -> register staging of one K slice (8 A + 8 B elements per thread)
-  T ra[8], rb[8];
+  // ---- global -> register staging of one K slice (SPA A + SPB B elements per thread)
+  // B slice [BK][BN]: element idx = e*NT + tid -> (k = e*(NT/BN) + tid/BN, n = tid%BN)
+  // A slice K-major [BK][BM]: (k = e*(NT/BM) + tid/BM, i = tid%BM); row-major A: (i = idx/BK, k = idx%BK)
+  constexpr int KPB = NT / BN, KPA = NT / BM;  // k rows covered per staging step
+  const int bk_l = tid / BN, bn_l = tid % BN;
+  const int ak_l = tid / BM, am_l = tid % BM;
+  const bool b_col_ok = (n0 + bn_l) < g.N;
+  const bool a_col_ok = (m0 + am_l) < g.M;
+  const int b_voff = (bk_l * ldb + bn_l) * ES;
+  const int a_voff = (AL == 1) ? (ak_l * lda + am_l) * ES : 0;
+  T ra[CF::SPA], rb[CF::SPB];
   auto load_slice = [&](int64_t k0) {
+    __amdgpu_buffer_rsrc_t rbr = rsrc(B + k0 * g.ldb + n0);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int idx = e * NT + tid;
-      // B: [BK][BN], coalesced along n
-      {
-        const int kk = idx / BN, nn = idx % BN;
-        const int64_t gk = k0 + kk, gn = n0 + nn;
-        rb[e] = (gk < g.K && gn < g.N) ? B[gk * g.ldb + gn] : T(0);
+    for (int e = 0; e < CF::SPB; ++e) {
+      const int64_t gk = k0 + e * KPB + bk_l;
+      rb[e] = (gk < g.K && b_col_ok) ? bload<T>(rbr, b_voff, e * KPB * ldb * ES) : T(0);
+    }
+    if (AL == 1) {
+      __amdgpu_buffer_rsrc_t rar = rsrc(A + k0 * g.lda + m0);
+#pragma unroll
+      for (int e = 0; e < CF::SPA; ++e) {
+        const int64_t gk = k0 + e * KPA + ak_l;
+        ra[e] = (gk < g.K && a_col_ok) ? bload<T>(rar, a_voff, e * KPA * lda * ES) : T(0);
       }
-      if (AL == 1) {  // K-major A: At[k][i], coalesced along i
-        const int kk = idx / BM, ii = idx % BM;
-        const int64_t gk = k0 + kk, gi = m0 + ii;
-        ra[e] = (gk < g.K && gi < g.M) ? A[gk * g.lda + gi] : T(0);
-      } else {  // row-major A: A[i][k], 16 consecutive k per row
+    } else {
+      __amdgpu_buffer_rsrc_t rar = rsrc(A + m0 * g.lda + k0);
+#pragma unroll
+      for (int e = 0; e < CF::SPA; ++e) {
+        const int idx = e * NT + tid;
         const int ii = idx / BK, kk = idx % BK;
-        const int64_t gk = k0 + kk, gi = m0 + ii;
-        ra[e] = (gk < g.K && gi < g.M) ? A[gi * g.lda + gk] : T(0);
+        const bool ok = (k0 + kk) < g.K && (m0 + ii) < g.M;
+        ra[e] = ok ? bload<T>(rar, (ii * lda + kk) * ES, 0) : T(0);
       }
     }
   };
   auto store_slice = [&](int buf) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int idx = e * NT + tid;
-      lds[buf][1][idx / BN][idx % BN] = rb[e];
-      if (AL == 1)
-        lds[buf][0][idx / BM][idx % BM] = ra[e];
-      else
-        lds[buf][0][idx % BK][idx / BK] = ra[e];
+    for (int e = 0; e < CF::SPB; ++e) ldsB[buf][e * KPB + bk_l][bn_l] = rb[e];
+#pragma unroll
+    for (int e = 0; e < CF::SPA; ++e) {
+      if (AL == 1) {
+        ldsA[buf][e * KPA + ak_l][am_l] = ra[e];
+      } else {
+        const int idx = e * NT + tid;
+        ldsA[buf][idx % BK][idx / BK] = ra[e];
+      }
     }
   };
 
@@ -159,16 +246,16 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
     if (kt + 1 < nk) load_slice((int64_t)(kt + 1) * BK);
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
-      T a[4], b[4];
+      T a[MI], b[NJ];
       const int kr = kk + (lane >> 4);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = lds[cur][0][kr][wm * 64 + i * 16 + (lane & 15)];
+      for (int i = 0; i < MI; ++i) a[i] = ldsA[cur][kr][wm * TM + i * 16 + (lane & 15)];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = lds[cur][1][kr][wn * 64 + j * 16 + (lane & 15)];
+      for (int j = 0; j < NJ; ++j) b[j] = ldsB[cur][kr][wn * TN + j * 16 + (lane & 15)];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = MF::op(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < NJ; ++j) acc[i][j] = MF::op(a[i], b[j], acc[i][j]);
     }
     if (kt + 1 < nk) store_slice(cur ^ 1);
     __syncthreads();
@@ -176,59 +263,105 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
 
   if (MODE == MODE_ACC || MODE == MODE_STORE) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t col = n0 + wn * 64 + j * 16 + (lane & 15);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int64_t row = m0 + wm * 64 + i * 16 + MF::row_of(lane, q);
-          if (row < g.M && col < g.N) {
-            T v = acc[i][j][q];
-            if (MODE == MODE_ACC && row >= g.pr0 && row < g.pr0 + g.K) v = B[(row - g.pr0) * g.ldb + col];
-            C[row * g.ldc + col] = v;
-          }
-        }
-      }
-  } else {  // MODE_RESID: per-row partial sum of |acc - I| over this wave's 64 real columns
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int64_t row = m0 + wm * 64 + i * 16 + MF::row_of(lane, q);
+        const int r = rlane + i * 16 + MF::rq(q);
+        const int soff = (i * 16 + MF::rq(q)) * ldc * ES;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int c = clane + j * 16;
+          if (r < Mt && c < Nt) bstore(acc[i][j][q], rc, cvoff + j * 16 * ES, soff);
+        }
+      }
+    // Pivot block rows take R (= the B rows) verbatim.  Only the (rare, uniform) tiles that
+    // intersect the pivot block run this; each thread overwrites exactly the elements it stored
+    // above, so program order makes the second store win, and acc is dead here (no extra VGPRs
+    // live across the main loop).
+    if (MODE == MODE_ACC && p0 < p1) {
+      // B row (m0 + r - pr0) = r - plo.  The resource base absorbs -plo rows so the per-lane
+      // offset stays non-negative (buffer range checks treat the VGPR offset as unsigned).
+      __amdgpu_buffer_rsrc_t rbp = rsrc(B + n0 - plo * g.ldb);
+      const int bvoff = (rlane * ldb + clane) * ES;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = rlane + i * 16 + MF::rq(q);
+          const int soff = (i * 16 + MF::rq(q)) * ldc * ES;
+          const int bsoff = (i * 16 + MF::rq(q)) * ldb * ES;
+          if (r >= p0 && r < p1 && r < Mt) {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+              const int c = clane + j * 16;
+              if (c < Nt) bstore(bload<T>(rbp, bvoff + j * 16 * ES, bsoff), rc, cvoff + j * 16 * ES, soff);
+            }
+          }
+        }
+    }
+  } else {  // MODE_RESID: per-row partial sum of |acc - I| over this wave's TN real columns
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t row = m0 + rlane + i * 16 + MF::rq(q);
         const int64_t gr = ((row / g.blk_m) * g.p + g.k) * g.blk_m + row % g.blk_m;
         double s = 0.0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int64_t col = n0 + wn * 64 + j * 16 + (lane & 15);
-          if (col < g.n_real) {
-            const double v = (double)acc[i][j][q] - (col == gr ? 1.0 : 0.0);
-            s += fabs(v);
-          }
+        for (int j = 0; j < NJ; ++j) {
+          const int64_t col = n0 + clane + j * 16;
+          if (col < g.n_real) s += fabs((double)acc[i][j][q] - (col == gr ? 1.0 : 0.0));
         }
         // sum across the 16 lanes that share this row (lane & 15)
 #pragma unroll
         for (int off = 1; off < 16; off <<= 1) s += __shfl_xor(s, off, 64);
-        if ((lane & 15) == 0 && row < g.M)
-          g.partial[row * g.nparts + (int64_t)tn * 2 + wn] = s;
+        if ((lane & 15) == 0 && row < g.M) g.partial[row * g.nparts + (int64_t)tn * WN + wn] = s;
       }
   }
 }
 
-template <typename T, int AL, int MODE>
-static void launch(const GemmArgs& a0, hipStream_t s) {
+template <typename T, int AL, int MODE, typename CF>
+static void launch_cfg(const GemmArgs& a0, hipStream_t s) {
   GemmArgs a = a0;
-  a.tiles_m = (int)((a.M + BM - 1) / BM);
-  a.tiles_n = (int)((a.N + BN - 1) / BN);
+  a.tiles_m = (int)((a.M + CF::BM - 1) / CF::BM);
+  a.tiles_n = (int)((a.N + CF::BN - 1) / CF::BN);
   const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;
   if (nwg <= 0) return;
-  hipLaunchKernelGGL((gemm_kernel<T, AL, MODE>), dim3((unsigned)nwg), dim3(NT), 0, s, a);
+  hipLaunchKernelGGL((gemm_kernel<T, AL, MODE, CF>), dim3((unsigned)nwg), dim3(CF::NT), 0, s, a);
+}
+
+// Variant selection (GJ_GEMM_VARIANT=big|narrow|tall or set_gemm_variant(); default by measurement).
+static int g_variant = -1;
+static int gemm_variant() {
+  if (g_variant < 0) {
+    const char* e = getenv("GJ_GEMM_VARIANT");
+    g_variant = e ? gemm_variant_id(e) : 1;  // narrow: 4 WG/CU hides C latency best (bench_gemm)
+  }
+  return g_variant;
+}
+int gemm_variant_id(const char* name) {
+  const std::string s(name);
+  return s == "big" ? 0 : s == "tall" ? 2 : s == "valu" ? 3 : 1;
+}
+void set_gemm_variant(int v) { g_variant = v; }
+
+template <typename T, int AL, int MODE>
+static void launch(const GemmArgs& a, hipStream_t s) {
+  if (MODE == MODE_RESID) return launch_cfg<T, AL, MODE, CfgBig>(a, s);
+  switch (gemm_variant()) {
+    case 1: return launch_cfg<T, AL, MODE, CfgNarrow>(a, s);
+    case 2: return launch_cfg<T, AL, MODE, CfgTall>(a, s);
+    case 3: return launch_cfg<T, AL, MODE, CfgNarrow>(a, s);  // valu is fp64/K-major only
+    default: return launch_cfg<T, AL, MODE, CfgBig>(a, s);
+  }
 }
 
 void gemm(DType dt, int op, int a_kmajor, int64_t M, int64_t N, int64_t K, const void* A,
           int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, hipStream_t s,
           int64_t zc0, int64_t zc1, int64_t pr0) {
   if (M <= 0 || N <= 0) return;
+  if (dt == DType::F64 && a_kmajor && gemm_variant() == 3)
+    return gemm_valu(op, M, N, K, A, lda, B, ldb, C, ldc, s, zc0, zc1, pr0);
   GemmArgs a{};
   a.M = M; a.N = N; a.K = K; a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.C = C; a.ldc = ldc;
   a.zc0 = zc0; a.zc1 = zc1; a.pr0 = pr0 < 0 ? -(int64_t(1) << 62) : pr0;
@@ -249,7 +382,7 @@ void gemm(DType dt, int op, int a_kmajor, int64_t M, int64_t N, int64_t K, const
 #undef GJ_DISPATCH
 }
 
-int residual_nparts(int64_t N) { return (int)(((N + BN - 1) / BN) * 2); }
+int residual_nparts(int64_t N) { return (int)(((N + CfgBig::BN - 1) / CfgBig::BN) * CfgBig::WN); }
 
 void residual_partial(DType dt, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                       const void* B, int64_t ldb, int64_t n_real, int64_t blk_m, int64_t p,

@@ -16,6 +16,7 @@
 #include "gj/host_device.hpp"
 #include "gj/io.hpp"
 #include "gj/runner.hpp"
+#include "../kernels/kernels.hpp"
 
 namespace py = pybind11;
 using namespace gj;
@@ -117,6 +118,7 @@ PYBIND11_MODULE(_C, mod) {
     return n;
   });
   mod.def("rccl_unique_id", [] { return py::bytes(RcclComm::unique_id()); });
+  mod.def("set_gemm_variant", [](const std::string& v) { kern::set_gemm_variant(kern::gemm_variant_id(v.c_str())); });
 
   // Kernel-level entry points (raw pointers; used by the per-kernel numerics tests and
   // mpi_jordan_crazy_acceleration_amd.ops).  Every op runs on the MAIN stream and is waited for.

@@ -52,8 +52,10 @@ def test_fp32_engine(native):
     eng = native.Engine(native.hip_device(0), native.self_comm(), n, m, "fp32")
     eng.generate("random", 1)
     assert eng.solve()["status"] == 0
-    res = eng.residual_generated("random", 1)
-    assert res < 5e-2, res
+    inv = eng.download_local_rows()
+    ref = np.linalg.inv(generate_matrix(n, "random", 1))
+    rel = np.abs(inv - ref).max() / np.abs(ref).max()
+    assert rel < 5e-2, rel  # fp32: eps 6e-8 amplified by cond(A) ~ 1e4-1e5
 
 
 def test_singular_detected(native):
