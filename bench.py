@@ -37,6 +37,7 @@ def main() -> int:
     ap.add_argument("--gen", default="random")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--chunk-cols", type=int, default=0)
+    ap.add_argument("--depth", type=int, default=2, help="elimination steps fused per trailing update")
     ap.add_argument("--no-residual", action="store_true")
     ap.add_argument("--force-rccl", action="store_true", help="use the RCCL communicator even at 1 rank")
     ap.add_argument("--gemm-variant", default=None, help="big | narrow | tall (kernel tile config)")
@@ -70,7 +71,7 @@ def main() -> int:
     else:
         dev = C.hip_device(local)
         comm = C.self_comm()
-    eng = C.Engine(dev, comm, args.n, args.m, args.dtype, args.chunk_cols)
+    eng = C.Engine(dev, comm, args.n, args.m, args.dtype, args.chunk_cols, 1e-15, False, args.depth)
 
     def barrier():
         if dist.is_initialized():
@@ -127,6 +128,7 @@ def main() -> int:
                 "parallelism": f"block-row-cyclic p={world} (RCCL over xGMI)" if world > 1 else "single GPU",
                 "n": args.n,
                 "m": args.m,
+                "depth": args.depth,
             },
             "solve_seconds_max": round(inner_max, 4),
             "residual_inf": res,

@@ -22,6 +22,7 @@
 //   --print-max N        corner size (reference MAX_P = 10)
 //   --eps E              singularity threshold factor (reference EPS = 1e-15)
 //   --chunk-cols C       broadcast pipelining granularity
+//   --depth D            elimination steps fused per trailing update (1..4, default 2)
 //   --repeat R           time R solves, report the last (min also in --json)
 //   --out FILE           write the inverse (text, or .bin)
 //   --json               machine-readable report on stderr
@@ -101,6 +102,7 @@ int main(int argc, char* argv[]) {
       } else if (a == "--print-max") cfg.print_max = std::atoi(val("--print-max"));
       else if (a == "--eps") cfg.solve.eps = std::atof(val("--eps"));
       else if (a == "--chunk-cols") cfg.solve.chunk_cols = std::atoll(val("--chunk-cols"));
+      else if (a == "--depth") cfg.solve.depth = std::atoi(val("--depth"));
       else if (a == "--repeat") cfg.repeats = std::atoi(val("--repeat"));
       else if (a == "--out") out_file = val("--out");
       else if (a == "--json") json = true;

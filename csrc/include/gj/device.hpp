@@ -32,6 +32,16 @@ struct GenSpec {
 enum class GemmOp : int { Acc = 0, Store = 1 };
 enum class ALayout : int { RowMajor = 0, KMajor = 1 };
 
+// Elimination extras of GemmOp::Acc: C enters as 0 in the columns [zc0, zc1) (the pivot block
+// columns of the current panel) and in the row blocks [zr[i], zr[i] + zh) (its pivot rows).
+struct GemmExtra {
+  static constexpr int kMaxZeroRows = 4;
+  int64_t zc0 = 0, zc1 = 0;
+  int nzr = 0;
+  int64_t zr[kMaxZeroRows] = {0, 0, 0, 0};
+  int64_t zh = 0;
+};
+
 class Device {
  public:
   virtual ~Device() = default;
@@ -46,6 +56,7 @@ class Device {
   virtual void release_pinned(void* p) = 0;
   virtual size_t free_memory() const = 0;
   virtual void memset0(void* p, size_t bytes, int s) = 0;
+  virtual void memset2d(void* p, size_t pitch, size_t width_bytes, size_t height, int s) = 0;
   virtual void copy(void* dst, const void* src, size_t bytes, int s) = 0;
   virtual void copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width_bytes,
                       size_t height, int s) = 0;
@@ -87,11 +98,9 @@ class Device {
                             int s) = 0;
   // R[i*ldr + j] = H[i][j] = Ht[j*m + i]   (the pivot column block of the broadcast row).
   virtual void h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, int s) = 0;
-  // GemmOp::Acc extras (the elimination step): C columns [zc0, zc1) enter as 0, and rows
-  // [pr0, pr0 + K) are written with the corresponding rows of B instead of C + A*B (pr0 < 0: none).
   virtual void gemm(DType dt, GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const void* A,
                     int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int s,
-                    int64_t zc0 = 0, int64_t zc1 = 0, int64_t pr0 = -1) = 0;
+                    const GemmExtra& ex = GemmExtra()) = 0;
   // Finalisation gather: dst[(dst_blk[b]*m + r)*ldd + c*m + j] = X[(b*m + r)*ldx + colsrc[c]*m + j]
   // for local block b < nblk, destination column block c < Nr.
   virtual void permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx,

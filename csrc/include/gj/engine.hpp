@@ -20,6 +20,7 @@
 //     next pivot row chunk by chunk as soon as each column chunk of step t is finished.
 #pragma once
 
+#include <algorithm>
 #include <memory>
 #include <string>
 #include <vector>
@@ -32,6 +33,7 @@ namespace gj {
 struct SolveOptions {
   DType dtype = DType::F64;
   int64_t chunk_cols = 0;   // pipelining granularity of the pivot-row broadcast (0 = auto)
+  int depth = 2;            // elimination steps fused per trailing update (K = depth*m), 1..4
   double eps = kDefaultEps;
   bool sync_debug = false;  // synchronise every stream after every phase (race screening)
   bool profile = false;     // per-phase timing (adds synchronisation)
@@ -87,33 +89,52 @@ class Engine {
   int64_t real_local_rows() const;
 
  private:
+  static constexpr int kMaxDepth = GemmExtra::kMaxZeroRows;
   void alloc_buffers();
   void free_buffers();
-  void select(int64_t t);      // pivot search for column block t (SIDE stream)
-  void post_select(int64_t t, const PivotResult& r);
-  void normalize_and_bcast(int64_t t, const PivotResult& r, bool wait_main);
+  // Pivot search for step t on the multiplier segment Lt (SIDE stream); result -> piv_host_[t&1].
+  void select(int64_t t, const void* Lt);
+  // Panel factorisation (pivot searches of its q steps, panel pieces, then the chunk pipeline of
+  // the normalised pivot rows).  Returns false when the matrix is singular.
+  bool factor_panel(int64_t v, bool wait_main, SolveStats& st, double& host_wait);
+  void chunk_pipeline(int64_t v, bool wait_main);
+  void big_update(int64_t u);
   void finalize(const std::vector<int32_t>& seq);
   double residual_common();
   void dbg_sync();
   size_t esz() const { return dtype_size(opt_.dtype); }
   char* elem(void* base, int64_t off) const { return static_cast<char*>(base) + off * (int64_t)esz(); }
+  int64_t panel_t0(int64_t v) const { return v * d_; }
+  int64_t panel_q(int64_t v) const { return std::min<int64_t>(d_, L_.Nr - v * d_); }
+  int64_t npanels() const { return (L_.Nr + d_ - 1) / d_; }
+  // chunk c of the stacked-rows buffer: (d*m) x W block, ld W
+  char* rb_chunk(int par, int64_t c) const {
+    return elem(Rb_[par], (int64_t)d_ * L_.m * cb0_[c] * L_.m);
+  }
+  int64_t chunk_w(int64_t c) const { return (cb1_[c] - cb0_[c]) * L_.m; }
+  GemmExtra pivot_rows_extra(int par, int64_t nsteps) const;  // this rank's pivot rows of a panel
 
   Device& dev_;
   Comm& comm_;
   SolveOptions opt_;
   Layout L_;
+  int d_ = 1;
   double norm_a_ = -1;
 
-  // chunk plan (block-column ranges)
-  std::vector<int64_t> cb0_, cb1_;   // in blocks
+  // chunk plan (block-column ranges, multiples of d_ blocks so a panel never straddles chunks)
+  std::vector<int64_t> cb0_, cb1_;
   std::vector<int64_t> chunk_of_;    // block -> chunk
 
   // device buffers
   void* X_ = nullptr;       // input / working panel
   void* out_ = nullptr;     // result panel
-  void* Lt_[2] = {nullptr, nullptr};
-  void* R_[2] = {nullptr, nullptr};
-  void* Ht_[2] = {nullptr, nullptr};
+  void* At_[2] = {nullptr, nullptr};   // stacked K-major multipliers of a panel, (d*m) x rows
+  void* Rb_[2] = {nullptr, nullptr};   // stacked normalised pivot rows, chunk-major (d*m) x npad
+  void* PP_[2] = {nullptr, nullptr};   // panel pieces: R_t restricted to the panel's columns, (d*m) x (d*m)
+  void* Lrow_[2][kMaxDepth] = {};      // multipliers of pivot row s_t for earlier panel steps, K-major
+  void* Ht_[2][kMaxDepth] = {};        // H_t^T
+  void* T_ = nullptr;                  // row-update temp, m x Wmax
+  void* RP_ = nullptr;                 // panel-piece temp, m x (d*m)
   void* inv_ = nullptr;
   double* scores_ = nullptr;
   int32_t* valid_ = nullptr;
@@ -131,11 +152,13 @@ class Engine {
   int32_t* ihost_ = nullptr;
   double* dhost_ = nullptr;
   int64_t ihost_len_ = 0;
+  PivotResult piv_[2][kMaxDepth];      // pivots of the panels in flight (by panel parity)
 
   // events
-  int ev_L_ = -1, ev_sel_[2] = {-1, -1}, ev_adj_[2] = {-1, -1}, ev_main_ = -1, ev_comm_ = -1;
-  std::vector<int> ev_c_;        // per chunk: MAIN finished step t's chunk
-  std::vector<int> ev_b_[2];     // per chunk: R chunk broadcast complete
+  int ev_L_ = -1, ev_main_ = -1, ev_sel_[2] = {-1, -1}, ev_edit_[2] = {-1, -1};
+  int ev_pp_[2][kMaxDepth] = {};
+  std::vector<int> ev_c_;        // per chunk: MAIN finished the panel update of that chunk
+  std::vector<int> ev_b_[2];     // per chunk: all stacked rows of that chunk broadcast
   bool solved_ = false;
 };
 

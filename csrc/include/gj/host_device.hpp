@@ -17,6 +17,7 @@ class HostDevice : public Device {
   void release_pinned(void* p) override;
   size_t free_memory() const override;
   void memset0(void* p, size_t bytes, int s) override;
+  void memset2d(void* p, size_t pitch, size_t width_bytes, size_t height, int s) override;
   void copy(void* dst, const void* src, size_t bytes, int s) override;
   void copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width_bytes,
               size_t height, int s) override;
@@ -45,8 +46,8 @@ class HostDevice : public Device {
                     int32_t* used, int32_t* seq, PivotResult* out, int s) override;
   void h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, int s) override;
   void gemm(DType dt, GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const void* A,
-            int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int s, int64_t zc0 = 0,
-            int64_t zc1 = 0, int64_t pr0 = -1) override;
+            int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int s,
+            const GemmExtra& ex = GemmExtra()) override;
   void permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx, int64_t nblk,
                       int64_t m, int64_t Nr, const int32_t* dst_blk, const int32_t* colsrc,
                       int s) override;

@@ -2,8 +2,9 @@
 //
 //   MODE_ACC   : C[M x N] += A * B       (the elimination update, reference mult_substr_block
 //                                          main.cpp:151-206 called from the hot loop :1165-1194)
-//                with two fused extras: C columns [zc0, zc1) enter as 0 (pivot block column,
-//                X[i,t] := -L_i H) and rows [pr0, pr0 + K) are written with B (the pivot row R_t)
+//                with fused extras: C enters as 0 in columns [zc0, zc1) (the panel's pivot block
+//                columns, X[i,t] := sum -L_i H) and in up to 4 row blocks (the panel's pivot rows,
+//                whose multiplier rows the engine turned into [0 .. I .. L] coefficients)
 //   MODE_STORE : C[M x N]  = A * B       (pivot-row normalisation, reference mult_block
 //                                          main.cpp:888-950 called at :1136-1159)
 //   MODE_RESID : per-row partial sums of |A*B - I| (residual, reference matrix_mult_matrix +
@@ -113,9 +114,10 @@ struct GemmArgs {
   void* C;
   int64_t ldc;
   int tiles_m, tiles_n;
-  // MODE_ACC extras: C columns [zc0, zc1) enter as 0 (the pivot block column: X[i,t] := -L_i H),
-  // rows [pr0, pr0 + K) are the pivot block row: they are written with B (= R) instead of C + A*B.
-  int64_t zc0, zc1, pr0;
+  // MODE_ACC extras (see GemmExtra): zero-input columns [zc0, zc1) and row blocks [zr, zr + zh)
+  int64_t zc0, zc1;
+  int64_t zr[GemmExtra::kMaxZeroRows];
+  int64_t zh;
   // residual
   int64_t n_real, blk_m, p, k;
   double* partial;  // [M][nparts]
@@ -160,8 +162,13 @@ __global__ __launch_bounds__(CF::NT, CF::WAVES_PER_SIMD) void gemm_kernel(GemmAr
   const int Nt = (int)((g.N - n0) < BN ? (g.N - n0) : BN);
   const int64_t zlo = g.zc0 - n0, zhi = g.zc1 - n0;
   const int z0 = (int)(zlo < 0 ? 0 : (zlo > BN ? BN : zlo)), z1 = (int)(zhi < 0 ? 0 : (zhi > BN ? BN : zhi));
-  const int64_t plo = g.pr0 - m0, phi = g.pr0 + g.K - m0;
-  const int p0 = (int)(plo < 0 ? 0 : (plo > BM ? BM : plo)), p1 = (int)(phi < 0 ? 0 : (phi > BM ? BM : phi));
+  int zr0[GemmExtra::kMaxZeroRows], zr1[GemmExtra::kMaxZeroRows];
+#pragma unroll
+  for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) {
+    const int64_t lo = g.zr[z] - m0, hi = g.zr[z] + g.zh - m0;
+    zr0[z] = (int)(lo < 0 ? 0 : (lo > BM ? BM : lo));
+    zr1[z] = (int)(hi < 0 ? 0 : (hi > BM ? BM : hi));
+  }
   __amdgpu_buffer_rsrc_t rc = rsrc(MODE == MODE_RESID ? (const void*)A : (const void*)(C + m0 * g.ldc + n0));
   const int cvoff = (rlane * ldc + clane) * ES;
 
@@ -173,10 +180,13 @@ __global__ __launch_bounds__(CF::NT, CF::WAVES_PER_SIMD) void gemm_kernel(GemmAr
       for (int q = 0; q < 4; ++q) {
         const int r = rlane + i * 16 + MF::rq(q);
         const int soff = (i * 16 + MF::rq(q)) * ldc * ES;
+        bool zrow = false;
+#pragma unroll
+        for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) zrow |= (r >= zr0[z] && r < zr1[z]);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const int c = clane + j * 16;
-          const bool ok = r < Mt && c < Nt && !(c >= z0 && c < z1);
+          const bool ok = r < Mt && c < Nt && !zrow && !(c >= z0 && c < z1);
           acc[i][j][q] = ok ? bload<T>(rc, cvoff + j * 16 * ES, soff) : T(0);
         }
       }
@@ -274,31 +284,6 @@ __global__ __launch_bounds__(CF::NT, CF::WAVES_PER_SIMD) void gemm_kernel(GemmAr
           if (r < Mt && c < Nt) bstore(acc[i][j][q], rc, cvoff + j * 16 * ES, soff);
         }
       }
-    // Pivot block rows take R (= the B rows) verbatim.  Only the (rare, uniform) tiles that
-    // intersect the pivot block run this; each thread overwrites exactly the elements it stored
-    // above, so program order makes the second store win, and acc is dead here (no extra VGPRs
-    // live across the main loop).
-    if (MODE == MODE_ACC && p0 < p1) {
-      // B row (m0 + r - pr0) = r - plo.  The resource base absorbs -plo rows so the per-lane
-      // offset stays non-negative (buffer range checks treat the VGPR offset as unsigned).
-      __amdgpu_buffer_rsrc_t rbp = rsrc(B + n0 - plo * g.ldb);
-      const int bvoff = (rlane * ldb + clane) * ES;
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int r = rlane + i * 16 + MF::rq(q);
-          const int soff = (i * 16 + MF::rq(q)) * ldc * ES;
-          const int bsoff = (i * 16 + MF::rq(q)) * ldb * ES;
-          if (r >= p0 && r < p1 && r < Mt) {
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-              const int c = clane + j * 16;
-              if (c < Nt) bstore(bload<T>(rbp, bvoff + j * 16 * ES, bsoff), rc, cvoff + j * 16 * ES, soff);
-            }
-          }
-        }
-    }
   } else {  // MODE_RESID: per-row partial sum of |acc - I| over this wave's TN real columns
 #pragma unroll
     for (int i = 0; i < MI; ++i)
@@ -356,15 +341,23 @@ static void launch(const GemmArgs& a, hipStream_t s) {
   }
 }
 
+static void fill_extra(GemmArgs& a, const GemmExtra* ex) {
+  constexpr int64_t kNone = -(int64_t(1) << 62);
+  a.zc0 = ex ? ex->zc0 : 0;
+  a.zc1 = ex ? ex->zc1 : 0;
+  a.zh = ex ? ex->zh : 0;
+  for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) a.zr[z] = (ex && z < ex->nzr) ? ex->zr[z] : kNone;
+}
+
 void gemm(DType dt, int op, int a_kmajor, int64_t M, int64_t N, int64_t K, const void* A,
           int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, hipStream_t s,
-          int64_t zc0, int64_t zc1, int64_t pr0) {
+          const GemmExtra* ex) {
   if (M <= 0 || N <= 0) return;
   if (dt == DType::F64 && a_kmajor && gemm_variant() == 3)
-    return gemm_valu(op, M, N, K, A, lda, B, ldb, C, ldc, s, zc0, zc1, pr0);
+    return gemm_valu(op, M, N, K, A, lda, B, ldb, C, ldc, s, ex);
   GemmArgs a{};
   a.M = M; a.N = N; a.K = K; a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.C = C; a.ldc = ldc;
-  a.zc0 = zc0; a.zc1 = zc1; a.pr0 = pr0 < 0 ? -(int64_t(1) << 62) : pr0;
+  fill_extra(a, ex);
   const int mode = op == 0 ? MODE_ACC : MODE_STORE;
 #define GJ_DISPATCH(T)                                                        \
   if (a_kmajor) {                                                             \
@@ -390,7 +383,7 @@ void residual_partial(DType dt, int64_t M, int64_t N, int64_t K, const void* A, 
   if (M <= 0 || N <= 0) return;
   GemmArgs a{};
   a.M = M; a.N = N; a.K = K; a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.C = nullptr; a.ldc = 0;
-  a.zc0 = a.zc1 = 0; a.pr0 = -(int64_t(1) << 62);
+  fill_extra(a, nullptr);
   a.n_real = n_real; a.blk_m = blk_m; a.p = p; a.k = k; a.partial = partial;
   a.nparts = residual_nparts(N);
   if (dt == DType::F64)

@@ -47,7 +47,9 @@ struct VArgs {
   double* C;
   int64_t ldc;
   int tiles_m, tiles_n;
-  int64_t zc0, zc1, pr0;
+  int64_t zc0, zc1;
+  int64_t zr[GemmExtra::kMaxZeroRows];
+  int64_t zh;
   int store;  // 1: C = A*B, 0: C += A*B
 };
 
@@ -65,8 +67,13 @@ __global__ __launch_bounds__(VNT, 2) void gemm_valu_f64(VArgs g) {
   const int Nt = (int)((g.N - n0) < VBN ? (g.N - n0) : VBN);
   const int64_t zlo = g.zc0 - n0, zhi = g.zc1 - n0;
   const int z0 = (int)(zlo < 0 ? 0 : (zlo > VBN ? VBN : zlo)), z1 = (int)(zhi < 0 ? 0 : (zhi > VBN ? VBN : zhi));
-  const int64_t plo = g.pr0 - m0, phi = g.pr0 + g.K - m0;
-  const int p0 = (int)(plo < 0 ? 0 : (plo > VBM ? VBM : plo)), p1 = (int)(phi < 0 ? 0 : (phi > VBM ? VBM : phi));
+  int zr0[GemmExtra::kMaxZeroRows], zr1[GemmExtra::kMaxZeroRows];
+#pragma unroll
+  for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) {
+    const int64_t lo = g.zr[z] - m0, hi = g.zr[z] + g.zh - m0;
+    zr0[z] = (int)(lo < 0 ? 0 : (lo > VBM ? VBM : lo));
+    zr1[z] = (int)(hi < 0 ? 0 : (hi > VBM ? VBM : hi));
+  }
 
   __amdgpu_buffer_rsrc_t rc = vrsrc(g.C + m0 * g.ldc + n0);
   const int cvoff = ((ty * 8) * ldc + tx) * 8;
@@ -74,13 +81,18 @@ __global__ __launch_bounds__(VNT, 2) void gemm_valu_f64(VArgs g) {
   double acc[8][8];
   if (!g.store) {
 #pragma unroll
-    for (int r = 0; r < 8; ++r)
+    for (int r = 0; r < 8; ++r) {
+      const int rr = ty * 8 + r;
+      bool zrow = false;
+#pragma unroll
+      for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) zrow |= (rr >= zr0[z] && rr < zr1[z]);
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
-        const int rr = ty * 8 + r, cc = tx + 16 * c;
-        const bool ok = rr < Mt && cc < Nt && !(cc >= z0 && cc < z1);
+        const int cc = tx + 16 * c;
+        const bool ok = rr < Mt && cc < Nt && !zrow && !(cc >= z0 && cc < z1);
         acc[r][c] = ok ? vload(rc, cvoff + c * 16 * 8, r * ldc * 8) : 0.0;
       }
+    }
   } else {
 #pragma unroll
     for (int r = 0; r < 8; ++r)
@@ -146,25 +158,10 @@ __global__ __launch_bounds__(VNT, 2) void gemm_valu_f64(VArgs g) {
       const int rr = ty * 8 + r, cc = tx + 16 * c;
       if (rr < Mt && cc < Nt) vstore(acc[r][c], rc, cvoff + c * 16 * 8, r * ldc * 8);
     }
-  if (!g.store && p0 < p1) {  // pivot block rows take B rows verbatim (see gemm.hip)
-    __amdgpu_buffer_rsrc_t rbp = vrsrc(g.B + n0 - plo * g.ldb);
-    const int bvoff = ((ty * 8) * ldb + tx) * 8;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int rr = ty * 8 + r;
-      if (rr >= p0 && rr < p1 && rr < Mt) {
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          const int cc = tx + 16 * c;
-          if (cc < Nt) vstore(vload(rbp, bvoff + c * 16 * 8, r * ldb * 8), rc, cvoff + c * 16 * 8, r * ldc * 8);
-        }
-      }
-    }
-  }
 }
 
 void gemm_valu(int op, int64_t M, int64_t N, int64_t K, const void* At, int64_t lda, const void* B,
-               int64_t ldb, void* C, int64_t ldc, hipStream_t s, int64_t zc0, int64_t zc1, int64_t pr0) {
+               int64_t ldb, void* C, int64_t ldc, hipStream_t s, const GemmExtra* ex) {
   if (M <= 0 || N <= 0) return;
   VArgs a{};
   a.M = M; a.N = N; a.K = K;
@@ -173,7 +170,11 @@ void gemm_valu(int op, int64_t M, int64_t N, int64_t K, const void* At, int64_t 
   a.C = static_cast<double*>(C); a.ldc = ldc;
   a.tiles_m = (int)((M + VBM - 1) / VBM);
   a.tiles_n = (int)((N + VBN - 1) / VBN);
-  a.zc0 = zc0; a.zc1 = zc1; a.pr0 = pr0 < 0 ? -(int64_t(1) << 62) : pr0;
+  constexpr int64_t kNone = -(int64_t(1) << 62);
+  a.zc0 = ex ? ex->zc0 : 0;
+  a.zc1 = ex ? ex->zc1 : 0;
+  a.zh = ex ? ex->zh : 0;
+  for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) a.zr[z] = (ex && z < ex->nzr) ? ex->zr[z] : kNone;
   a.store = op == 1;
   hipLaunchKernelGGL(gemm_valu_f64, dim3((unsigned)(a.tiles_m * a.tiles_n)), dim3(VNT), 0, s, a);
 }

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include "gj/common.hpp"
+#include "gj/device.hpp"
 #include "gj/layout.hpp"
 #include "gj/pivot.hpp"
 
@@ -13,11 +14,11 @@ namespace kern {
 // gemm.hip
 void gemm(DType dt, int op /*0 acc, 1 store*/, int a_kmajor, int64_t M, int64_t N, int64_t K,
           const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
-          hipStream_t s, int64_t zc0 = 0, int64_t zc1 = 0, int64_t pr0 = -1);
+          hipStream_t s, const GemmExtra* ex = nullptr);
 int residual_nparts(int64_t N);
 // VALU fp64 variant (gemm_valu.hip), K-major A only
 void gemm_valu(int op, int64_t M, int64_t N, int64_t K, const void* At, int64_t lda, const void* B,
-               int64_t ldb, void* C, int64_t ldc, hipStream_t s, int64_t zc0, int64_t zc1, int64_t pr0);
+               int64_t ldb, void* C, int64_t ldc, hipStream_t s, const GemmExtra* ex);
 int gemm_variant_id(const char* name);  // big | narrow | tall | valu
 void set_gemm_variant(int v);
 void residual_partial(DType dt, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,

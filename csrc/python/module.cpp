@@ -131,15 +131,23 @@ PYBIND11_MODULE(_C, mod) {
       .def("gemm",
            [](Device& d, const std::string& dt, const std::string& op, bool a_kmajor, int64_t M,
               int64_t N, int64_t K, U A, int64_t lda, U B, int64_t ldb, U C, int64_t ldc, int64_t zc0,
-              int64_t zc1, int64_t pr0) {
+              int64_t zc1, std::vector<int64_t> zero_rows, int64_t zh) {
+             GemmExtra ex;
+             ex.zc0 = zc0;
+             ex.zc1 = zc1;
+             if (zero_rows.size() > (size_t)GemmExtra::kMaxZeroRows) throw std::invalid_argument("too many zero rows");
+             ex.nzr = (int)zero_rows.size();
+             for (size_t i = 0; i < zero_rows.size(); ++i) ex.zr[i] = zero_rows[i];
+             ex.zh = zh;
              d.gemm(parse_dtype(dt), op == "store" ? GemmOp::Store : GemmOp::Acc,
                     a_kmajor ? ALayout::KMajor : ALayout::RowMajor, M, N, K, (const void*)A, lda,
-                    (const void*)B, ldb, (void*)C, ldc, S_MAIN, zc0, zc1, pr0);
+                    (const void*)B, ldb, (void*)C, ldc, S_MAIN, ex);
              d.sync_stream(S_MAIN);
            },
            py::arg("dtype"), py::arg("op"), py::arg("a_kmajor"), py::arg("M"), py::arg("N"), py::arg("K"),
            py::arg("A"), py::arg("lda"), py::arg("B"), py::arg("ldb"), py::arg("C"), py::arg("ldc"),
-           py::arg("zc0") = 0, py::arg("zc1") = 0, py::arg("pr0") = -1)
+           py::arg("zc0") = 0, py::arg("zc1") = 0, py::arg("zero_rows") = std::vector<int64_t>(),
+           py::arg("zh") = 0)
       .def("generate",
            [lay](Device& d, const std::string& dt, U X, int64_t n, int64_t m, int64_t p, int64_t k,
                  const std::string& kind, uint64_t seed) {
@@ -210,9 +218,11 @@ PYBIND11_MODULE(_C, mod) {
   };
   py::class_<PyEngine>(mod, "Engine")
       .def(py::init([](std::shared_ptr<Device> dev, std::shared_ptr<Comm> comm, int64_t n, int64_t m,
-                       const std::string& dtype, int64_t chunk_cols, double eps, bool sync_debug) {
+                       const std::string& dtype, int64_t chunk_cols, double eps, bool sync_debug,
+                       int depth) {
              SolveOptions o;
              o.dtype = parse_dtype(dtype);
+             o.depth = depth;
              o.chunk_cols = chunk_cols;
              o.eps = eps;
              o.sync_debug = sync_debug;
@@ -223,7 +233,8 @@ PYBIND11_MODULE(_C, mod) {
              return pe;
            }),
            py::arg("device"), py::arg("comm"), py::arg("n"), py::arg("m"), py::arg("dtype") = "fp64",
-           py::arg("chunk_cols") = 0, py::arg("eps") = kDefaultEps, py::arg("sync_debug") = false)
+           py::arg("chunk_cols") = 0, py::arg("eps") = kDefaultEps, py::arg("sync_debug") = false,
+           py::arg("depth") = 2)
       .def_property_readonly("layout",
                              [](PyEngine& e) {
                                const Layout& L = e.eng->layout();
@@ -315,6 +326,7 @@ PYBIND11_MODULE(_C, mod) {
     if (d.contains("chunk_cols")) c.solve.chunk_cols = d["chunk_cols"].cast<int64_t>();
     if (d.contains("eps")) c.solve.eps = d["eps"].cast<double>();
     if (d.contains("sync_debug")) c.solve.sync_debug = d["sync_debug"].cast<bool>();
+    if (d.contains("depth")) c.solve.depth = d["depth"].cast<int>();
     if (d.contains("residual")) {
       const std::string r = d["residual"].cast<std::string>();
       c.residual = r == "never" ? ResidualMode::Never : r == "compat" ? ResidualMode::Compat : ResidualMode::Always;

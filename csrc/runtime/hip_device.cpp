@@ -86,6 +86,9 @@ size_t HipDevice::free_memory() const {
 void HipDevice::memset0(void* p, size_t bytes, int s) {
   if (bytes) HIP_OK(hipMemsetAsync(p, 0, bytes, hs(streams_[s])));
 }
+void HipDevice::memset2d(void* p, size_t pitch, size_t w, size_t h, int s) {
+  if (w && h) HIP_OK(hipMemset2DAsync(p, pitch, 0, w, h, hs(streams_[s])));
+}
 void HipDevice::copy(void* dst, const void* src, size_t bytes, int s) {
   if (bytes && dst != src)
     HIP_OK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, hs(streams_[s])));
@@ -185,9 +188,9 @@ void HipDevice::h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t 
 }
 void HipDevice::gemm(DType dt, GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const void* A,
                      int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int s,
-                     int64_t zc0, int64_t zc1, int64_t pr0) {
+                     const GemmExtra& ex) {
   kern::gemm(dt, op == GemmOp::Acc ? 0 : 1, al == ALayout::KMajor ? 1 : 0, M, N, K, A, lda, B, ldb,
-             C, ldc, hs(streams_[s]), zc0, zc1, pr0);
+             C, ldc, hs(streams_[s]), &ex);
   check_launch();
 }
 void HipDevice::permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx,

@@ -46,13 +46,10 @@ const T* tp(const void* p) {
 
 template <typename T>
 void gemm_t(GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const T* A, int64_t lda,
-            const T* B, int64_t ldb, T* C, int64_t ldc, int nthreads, int64_t zc0, int64_t zc1,
-            int64_t pr0) {
+            const T* B, int64_t ldb, T* C, int64_t ldc, int nthreads, const GemmExtra& ex) {
   parallel_for(M, nthreads, [&](int64_t i) {
-    if (op == GemmOp::Acc && pr0 >= 0 && i >= pr0 && i < pr0 + K) {
-      for (int64_t j = 0; j < N; ++j) C[i * ldc + j] = B[(i - pr0) * ldb + j];
-      return;
-    }
+    bool zrow = false;
+    for (int z = 0; z < ex.nzr; ++z) zrow |= (i >= ex.zr[z] && i < ex.zr[z] + ex.zh);
     std::vector<double> acc(N, 0.0);
     for (int64_t k = 0; k < K; ++k) {
       const double a = (al == ALayout::RowMajor) ? (double)A[i * lda + k] : (double)A[k * lda + i];
@@ -63,7 +60,7 @@ void gemm_t(GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const T* A, 
     T* c = C + i * ldc;
     if (op == GemmOp::Acc)
       for (int64_t j = 0; j < N; ++j)
-        c[j] = (T)((j >= zc0 && j < zc1 ? 0.0 : (double)c[j]) + acc[j]);
+        c[j] = (T)((zrow || (j >= ex.zc0 && j < ex.zc1) ? 0.0 : (double)c[j]) + acc[j]);
     else
       for (int64_t j = 0; j < N; ++j) c[j] = (T)acc[j];
   });
@@ -120,6 +117,9 @@ void* HostDevice::alloc_pinned(size_t bytes) { return alloc(bytes); }
 void HostDevice::release_pinned(void* p) { std::free(p); }
 size_t HostDevice::free_memory() const { return ~size_t(0); }
 void HostDevice::memset0(void* p, size_t bytes, int) { std::memset(p, 0, bytes); }
+void HostDevice::memset2d(void* p, size_t pitch, size_t w, size_t h, int) {
+  for (size_t r = 0; r < h; ++r) std::memset(static_cast<char*>(p) + r * pitch, 0, w);
+}
 void HostDevice::copy(void* dst, const void* src, size_t bytes, int) {
   if (dst != src) std::memmove(dst, src, bytes);
 }
@@ -277,14 +277,14 @@ void HostDevice::h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t
 
 void HostDevice::gemm(DType dt, GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K,
                       const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc,
-                      int, int64_t zc0, int64_t zc1, int64_t pr0) {
+                      int, const GemmExtra& ex) {
   if (M <= 0 || N <= 0) return;
   if (dt == DType::F64)
     gemm_t<double>(op, al, M, N, K, tp<double>(A), lda, tp<double>(B), ldb, tp<double>(C), ldc,
-                   nthreads_, zc0, zc1, pr0);
+                   nthreads_, ex);
   else
     gemm_t<float>(op, al, M, N, K, tp<float>(A), lda, tp<float>(B), ldb, tp<float>(C), ldc,
-                  nthreads_, zc0, zc1, pr0);
+                  nthreads_, ex);
 }
 
 void HostDevice::permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx,

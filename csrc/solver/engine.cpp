@@ -5,10 +5,20 @@
 //   pivot search        :1039-1066 -> select(): Device::block_inverse + pivot_local
 //   MPI_Allreduce(piv)  :1074     -> Comm::allgather of 32-B records + Device::pivot_global
 //   singular exit       :1075-1083 -> Status::Singular on every rank at the same step
-//   gather_row + Bcast  :1093-1097 -> normalize_and_bcast(): owner normalises, chunked broadcast
+//   gather_row + Bcast  :1093-1097 -> chunk_pipeline(): owner normalises, chunked broadcast
 //   row swap            :1100-1131 -> none per step (logical bookkeeping) + finalize() once
 //   normalise (replicated on all ranks) :1132-1159 -> once, on the owner, as an MFMA GEMM
-//   eliminate           :1165-1194 -> Device::gemm(Acc) over every local row, chunked by columns
+//   eliminate           :1165-1194 -> big_update(): one MFMA GEMM of depth d*m per panel of d steps
+//
+// Panel algebra (steps t0..t0+q-1 of panel v, sequential semantics of the in-place sweep):
+//   L_t = -X^(t)[:, t],  R_t = H_t X^(t)[s_t, :] with R_t[t] := H_t,  H_t = inv(X^(t)[s_t, t])
+//   X^(t+1)[i, c] = X^(t)[i, c] + L_t[i] R_t[c]   (c != t, i != s_t)
+//   X^(t+1)[i, t] = L_t[i] H_t ,  X^(t+1)[s_t, :] = R_t
+// Unrolled over the panel this is ONE update  X += [L_t0 .. L_t1] [R_t0; ..; R_t1]  provided
+//   * the panel's own block columns enter as 0 and R_t'[t] := 0 for t' < t inside the panel,
+//   * the panel's pivot rows enter as 0 and their multiplier rows become [0 .. 0, I, L_t'' ..],
+// which is exactly what the GEMM extras (zero columns / zero rows) and the owner-side edits do.
+// Nothing cancels (no I + H tricks), so the numerics match the step-by-step reference.
 #include "gj/engine.hpp"
 
 #include <algorithm>
@@ -29,11 +39,13 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   GJ_REQUIRE(n > 0 && m > 0, "n and m must be positive");
   L_ = Layout::make(n, m, comm.size(), comm.rank());
   GJ_REQUIRE(L_.Nr < (int64_t(1) << 31), "too many block rows");
+  d_ = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)opt_.depth, (int64_t)kMaxDepth, L_.Nr}));
 
-  // Column chunk plan: fixed partition of the Nr block columns.
+  // Column chunk plan: fixed partition of the Nr block columns into runs of a multiple of d blocks.
   int64_t target_cols = opt_.chunk_cols;
   if (target_cols <= 0) target_cols = std::max<int64_t>(2048, (L_.npad + 7) / 8);
   int64_t cw = std::max<int64_t>(1, target_cols / m);
+  cw = ((cw + d_ - 1) / d_) * d_;
   for (int64_t b = 0; b < L_.Nr; b += cw) {
     cb0_.push_back(b);
     cb1_.push_back(std::min(L_.Nr, b + cw));
@@ -54,11 +66,13 @@ int64_t Engine::real_local_rows() const {
 }
 
 void Engine::alloc_buffers() {
-  const int64_t m = L_.m, rows = std::max<int64_t>(L_.rows, 1), npad = L_.npad;
+  const int64_t m = L_.m, rows = std::max<int64_t>(L_.rows, 1), npad = L_.npad, dm = (int64_t)d_ * m;
   const size_t es = esz();
   const size_t panel = (size_t)rows * npad * es;
-  const size_t need = 2 * panel + 2 * (size_t)m * rows * es + 2 * (size_t)m * npad * es +
-                      (size_t)std::max<int64_t>(L_.nblk, 1) * m * m * es;
+  int64_t wmax = 0;
+  for (size_t c = 0; c < cb0_.size(); ++c) wmax = std::max(wmax, chunk_w((int64_t)c));
+  const size_t need = 2 * panel + 2 * (size_t)dm * rows * es + 2 * (size_t)dm * npad * es +
+                      (size_t)std::max<int64_t>(L_.nblk, 1) * m * m * es + (size_t)m * wmax * es;
   if (dev_.on_gpu()) {
     size_t avail = dev_.free_memory();
     if (need + (64u << 20) > avail)
@@ -68,10 +82,16 @@ void Engine::alloc_buffers() {
   X_ = dev_.alloc(panel);
   out_ = dev_.alloc(panel);
   for (int i = 0; i < 2; ++i) {
-    Lt_[i] = dev_.alloc((size_t)m * rows * es);
-    R_[i] = dev_.alloc((size_t)m * npad * es);
-    Ht_[i] = dev_.alloc((size_t)m * m * es);
+    At_[i] = dev_.alloc((size_t)dm * rows * es);
+    Rb_[i] = dev_.alloc((size_t)dm * npad * es);
+    PP_[i] = dev_.alloc((size_t)dm * dm * es);
+    for (int j = 0; j < d_; ++j) {
+      Lrow_[i][j] = dev_.alloc((size_t)std::max<int64_t>(j, 1) * m * m * es);
+      Ht_[i][j] = dev_.alloc((size_t)m * m * es);
+    }
   }
+  T_ = dev_.alloc((size_t)m * wmax * es);
+  RP_ = dev_.alloc((size_t)m * dm * es);
   inv_ = dev_.alloc((size_t)std::max<int64_t>(L_.nblk, 1) * m * m * es);
   scores_ = static_cast<double*>(dev_.alloc(sizeof(double) * std::max<int64_t>(L_.nblk, 1)));
   valid_ = static_cast<int32_t*>(dev_.alloc(sizeof(int32_t) * std::max<int64_t>(L_.nblk, 1)));
@@ -91,18 +111,27 @@ void Engine::alloc_buffers() {
 
   ev_L_ = dev_.create_event();
   ev_main_ = dev_.create_event();
-  ev_comm_ = dev_.create_event();
   for (int i = 0; i < 2; ++i) {
     ev_sel_[i] = dev_.create_event();
-    ev_adj_[i] = dev_.create_event();
+    ev_edit_[i] = dev_.create_event();
+    for (int j = 0; j < kMaxDepth; ++j) ev_pp_[i][j] = dev_.create_event();
     for (size_t c = 0; c < cb0_.size(); ++c) ev_b_[i].push_back(dev_.create_event());
   }
   for (size_t c = 0; c < cb0_.size(); ++c) ev_c_.push_back(dev_.create_event());
 }
 
 void Engine::free_buffers() {
-  void* dptrs[] = {X_, out_, Lt_[0], Lt_[1], R_[0], R_[1], Ht_[0], Ht_[1], inv_, scores_, valid_,
-                   pos_, phys_at_, used_, seq_, myrec_, recs_, piv_dev_, dscratch_, iscratch_};
+  std::vector<void*> dptrs = {X_, out_, T_, RP_, inv_, scores_, valid_, pos_, phys_at_, used_, seq_,
+                              myrec_, recs_, piv_dev_, dscratch_, iscratch_};
+  for (int i = 0; i < 2; ++i) {
+    dptrs.push_back(At_[i]);
+    dptrs.push_back(Rb_[i]);
+    dptrs.push_back(PP_[i]);
+    for (int j = 0; j < kMaxDepth; ++j) {
+      dptrs.push_back(Lrow_[i][j]);
+      dptrs.push_back(Ht_[i][j]);
+    }
+  }
   for (void* p : dptrs)
     if (p) dev_.release(p);
   if (piv_host_) dev_.release_pinned(piv_host_);
@@ -152,12 +181,11 @@ double Engine::norm_inf() {
 }
 
 // ---------------------------------------------------------------- pivot search (SIDE stream)
-void Engine::select(int64_t t) {
+void Engine::select(int64_t t, const void* Lt) {
   const int par = (int)(t & 1);
   const double thresh = opt_.eps * norm_a_;
   if (L_.nblk > 0)
-    dev_.block_inverse(opt_.dtype, Lt_[par], L_.rows, inv_, scores_, valid_, used_, L_, thresh,
-                       S_SIDE);
+    dev_.block_inverse(opt_.dtype, Lt, L_.rows, inv_, scores_, valid_, used_, L_, thresh, S_SIDE);
   dev_.pivot_local(scores_, valid_, used_, pos_, L_, myrec_, S_SIDE);
   comm_.allgather(dev_, myrec_, recs_, sizeof(PivotRec), S_SIDE);
   dev_.pivot_global(recs_, (int32_t)L_.p, (int32_t)t, pos_, phys_at_, used_, seq_, piv_dev_, S_SIDE);
@@ -166,41 +194,205 @@ void Engine::select(int64_t t) {
   dbg_sync();
 }
 
-// Owner of the pivot row: keep H = inv(P) (transposed) for the normalisation of step t.
-void Engine::post_select(int64_t t, const PivotResult& r) {
-  const int par = (int)(t & 1);
-  if (r.owner == L_.k) {
-    const int64_t sl = r.phys / L_.p;  // local block index of s_t
-    const int64_t m = L_.m;
-    dev_.copy(Ht_[par], elem(inv_, sl * m * m), (size_t)m * m * esz(), S_SIDE);
-  }
-  dev_.record(ev_adj_[par], S_SIDE);
-  dbg_sync();
+GemmExtra Engine::pivot_rows_extra(int par, int64_t nsteps) const {
+  GemmExtra ex;
+  ex.zh = L_.m;
+  for (int64_t j = 0; j < nsteps; ++j)
+    if (piv_[par][j].owner == L_.k) ex.zr[ex.nzr++] = (piv_[par][j].phys / L_.p) * L_.m;
+  return ex;
 }
 
-// COMM stream: chunk by chunk, the owner forms R_t = H * X[s_t, :] (block t -> H) and every rank
-// takes part in the broadcast of that chunk.
-void Engine::normalize_and_bcast(int64_t t, const PivotResult& r, bool wait_main) {
-  const int par = (int)(t & 1);
-  const int64_t m = L_.m;
-  const bool owner = (r.owner == L_.k);
+// Pivot searches of panel v.  Column t0 is ready (extracted into At[par] segment 0, event ev_L_);
+// every later column of the panel is brought up to date on the SIDE stream from the broadcast
+// panel pieces.  For every step: owner edits (Lrow save, H, multiplier rows -> [0..I]), then the
+// panel piece PP_t = H_t X^(t)[s_t, panel columns] on COMM and its (small) broadcast.
+bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& host_wait) {
+  const int par = (int)(v & 1);
+  const int64_t m = L_.m, rows = L_.rows, npad = L_.npad, dm = (int64_t)d_ * m;
+  const int64_t t0 = panel_t0(v), q = panel_q(v);
+  const size_t es = esz();
+  for (int64_t j = 0; j < q; ++j) {
+    const int64_t t = t0 + j;
+    void* Lt = elem(At_[par], j * m * rows);
+    if (j == 0) {
+      dev_.wait(S_SIDE, ev_L_);
+    } else {
+      // column t after panel v-1 (look-ahead) and steps t0..t-1 of this panel
+      dev_.wait(S_SIDE, ev_pp_[par][j - 1]);
+      if (rows > 0) {
+        GemmExtra ex = pivot_rows_extra(par, j);
+        dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, m, j * m, At_[par], rows,
+                  elem(PP_[par], j * m), dm, elem(X_, t * m), npad, S_SIDE, ex);
+        dev_.extract_neg_t(opt_.dtype, Lt, rows, X_, npad, rows, t * m, m, S_SIDE);
+      }
+    }
+    select(t, Lt);
+    {
+      const double w0 = now_s();
+      dev_.sync_event(ev_sel_[t & 1]);
+      host_wait += now_s() - w0;
+    }
+    const PivotResult r = piv_host_[t & 1];
+    if (!r.found) {
+      dev_.sync_all();
+      st.status = Status::Singular;
+      st.singular_step = t;
+      return false;
+    }
+    piv_[par][j] = r;
+    st.pivots[t] = r.phys;
+    const bool owner = (r.owner == L_.k);
+    const int64_t sl = r.phys / L_.p;
+    if (owner) {
+      st.bcast_bytes += double(m) * npad * es;
+      if (j > 0)  // multipliers of row s_t for steps t0..t-1 (K-major j*m x m)
+        dev_.copy2d(Lrow_[par][j], m * es, elem(At_[par], sl * m), rows * es, m * es, j * m, S_SIDE);
+      dev_.copy(Ht_[par][j], elem(inv_, sl * m * m), (size_t)m * m * es, S_SIDE);
+      // multiplier rows of s_t: earlier segments -> 0, own segment -> I
+      dev_.memset2d(elem(At_[par], sl * m), rows * es, m * es, (j + 1) * m, S_SIDE);
+      dev_.add_diag(opt_.dtype, elem(At_[par], j * m * rows + sl * m), rows, m, 1.0, S_SIDE);
+    }
+    dev_.record(ev_edit_[par], S_SIDE);
+    dbg_sync();
+
+    // panel piece PP_t (m x q*m, ld dm) on COMM
+    dev_.wait(S_COMM, ev_edit_[par]);
+    void* pp = elem(PP_[par], j * m * dm);
+    if (owner) {
+      for (int64_t jc = 0; jc < q; ++jc) {
+        if (jc == j) continue;
+        void* rp = elem(RP_, jc * m);
+        if (jc < j) {  // earlier pivot column: sum over steps jc..j-1 only, no input
+          dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, m, (j - jc) * m,
+                    elem(Lrow_[par][j], jc * m * m), m, elem(PP_[par], jc * m * dm + jc * m), dm, rp,
+                    dm, S_COMM);
+        } else {  // later panel column: look-ahead value + all earlier steps
+          dev_.copy2d(rp, dm * es, elem(X_, sl * m * npad + (t0 + jc) * m), npad * es, m * es, m,
+                      S_COMM);
+          if (j > 0)
+            dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, m, m, j * m, Lrow_[par][j], m,
+                      elem(PP_[par], jc * m), dm, rp, dm, S_COMM);
+        }
+      }
+      dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, q * m, m, Ht_[par][j], m, RP_, dm, pp,
+                dm, S_COMM);
+      dev_.h_block(opt_.dtype, elem(pp, j * m), dm, Ht_[par][j], m, S_COMM);
+    }
+    comm_.bcast(dev_, pp, (size_t)m * dm * es, r.owner, S_COMM);
+    dev_.record(ev_pp_[par][j], S_COMM);
+    dbg_sync();
+  }
+  chunk_pipeline(v, wait_main);
+  return true;
+}
+
+// COMM stream: for every column chunk (in the order MAIN will consume them) and every step of
+// panel v, the owner of s_t forms R_t[chunk] = H_t (X[s_t, chunk] + Lrow_t R_prev[chunk]) outside
+// the panel's columns (those come from the panel piece, later panel blocks zeroed), then all
+// ranks broadcast that stacked row segment.
+void Engine::chunk_pipeline(int64_t v, bool wait_main) {
+  const int par = (int)(v & 1);
+  const int64_t m = L_.m, npad = L_.npad;
+  const int64_t t0 = panel_t0(v), q = panel_q(v);
+  const size_t es = esz();
   const int64_t C = (int64_t)cb0_.size();
-  const int64_t start = chunk_of_[t];
-  dev_.wait(S_COMM, ev_adj_[par]);
+  const bool has_next = (v + 1 < npanels());
+  const int64_t start = has_next ? chunk_of_[panel_t0(v + 1)] : 0;
+  const int64_t pc0 = t0 * m, pc1 = (t0 + q) * m;  // panel columns
   for (int64_t i = 0; i < C; ++i) {
     const int64_t c = (start + i) % C;
     const int64_t c0 = cb0_[c] * m, c1 = cb1_[c] * m, W = c1 - c0;
-    void* Rc = elem(R_[par], m * c0);
-    if (owner) {
-      if (wait_main) dev_.wait(S_COMM, ev_c_[c]);
-      const int64_t sl = r.phys / L_.p;
-      dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, W, m, Ht_[par], m,
-                elem(X_, sl * m * L_.npad + c0), L_.npad, Rc, W, S_COMM);
-      if (t >= cb0_[c] && t < cb1_[c])
-        dev_.h_block(opt_.dtype, elem(Rc, t * m - c0), W, Ht_[par], m, S_COMM);
+    if (wait_main) dev_.wait(S_COMM, ev_c_[c]);
+    int64_t ra[2], rb[2], nr = 0;
+    const bool has_panel = (pc0 >= c0 && pc0 < c1);
+    if (has_panel) {
+      if (pc0 > c0) { ra[nr] = c0; rb[nr] = pc0; ++nr; }
+      if (c1 > pc1) { ra[nr] = pc1; rb[nr] = c1; ++nr; }
+    } else {
+      ra[0] = c0; rb[0] = c1; nr = 1;
     }
-    comm_.bcast(dev_, Rc, (size_t)m * W * esz(), r.owner, S_COMM);
+    char* chunk = rb_chunk(par, c);
+    for (int64_t j = 0; j < q; ++j) {
+      const PivotResult& r = piv_[par][j];
+      char* seg = chunk + j * m * W * (int64_t)es;
+      if (r.owner == L_.k) {
+        const int64_t sl = r.phys / L_.p;
+        for (int64_t z = 0; z < nr; ++z) {
+          const int64_t a = ra[z], w = rb[z] - ra[z];
+          if (j == 0) {
+            dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, w, m, Ht_[par][j], m,
+                      elem(X_, sl * m * npad + a), npad, seg + (a - c0) * (int64_t)es, W, S_COMM);
+          } else {
+            dev_.copy2d(T_, W * es, elem(X_, sl * m * npad + a), npad * es, w * es, m, S_COMM);
+            dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, m, w, j * m, Lrow_[par][j], m,
+                      chunk + (a - c0) * (int64_t)es, W, T_, W, S_COMM);
+            dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, w, m, Ht_[par][j], m, T_, W,
+                      seg + (a - c0) * (int64_t)es, W, S_COMM);
+          }
+        }
+        if (has_panel) {  // panel columns: PP_t for blocks <= t, zero for later panel blocks
+          char* dst = seg + (pc0 - c0) * (int64_t)es;
+          dev_.copy2d(dst, W * es, elem(PP_[par], j * m * (int64_t)d_ * m), (int64_t)d_ * m * es,
+                      (j + 1) * m * es, m, S_COMM);
+          if (j + 1 < q)
+            dev_.memset2d(dst + (j + 1) * m * (int64_t)es, W * es, (q - j - 1) * m * es, m, S_COMM);
+        }
+      }
+      comm_.bcast(dev_, seg, (size_t)m * W * es, r.owner, S_COMM);
+    }
     dev_.record(ev_b_[par][c], S_COMM);
+  }
+  dbg_sync();
+}
+
+// MAIN stream: the depth-q trailing update of panel u.  The next panel's block columns are done
+// first (look-ahead) so its pivot search can start; then every other chunk.
+void Engine::big_update(int64_t u) {
+  const int par = (int)(u & 1), npar = par ^ 1;
+  const int64_t m = L_.m, rows = L_.rows, npad = L_.npad;
+  const int64_t t0 = panel_t0(u), q = panel_q(u), K = q * m;
+  const int64_t C = (int64_t)cb0_.size();
+  const bool has_next = (u + 1 < npanels());
+  const GemmExtra prows = pivot_rows_extra(par, q);
+  dev_.wait(S_MAIN, ev_edit_[par]);
+  int64_t x0 = -1, x1 = -1;  // look-ahead columns
+  if (has_next) {
+    const int64_t tn = panel_t0(u + 1), qn = panel_q(u + 1), cn = chunk_of_[tn];
+    x0 = tn * m;
+    x1 = (tn + qn) * m;
+    dev_.wait(S_MAIN, ev_b_[par][cn]);
+    if (rows > 0) {
+      dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, x1 - x0, K, At_[par], rows,
+                rb_chunk(par, cn) + (x0 - cb0_[cn] * m) * (int64_t)esz(), chunk_w(cn), elem(X_, x0),
+                npad, S_MAIN, prows);
+      dev_.extract_neg_t(opt_.dtype, At_[npar], rows, X_, npad, rows, x0, m, S_MAIN);
+    }
+    dev_.record(ev_L_, S_MAIN);
+    dbg_sync();
+  }
+  const int64_t start = has_next ? chunk_of_[panel_t0(u + 1)] : 0;
+  const int64_t pc0 = t0 * m, pc1 = (t0 + q) * m;
+  for (int64_t i = 0; i < C; ++i) {
+    const int64_t c = (start + i) % C;
+    const int64_t c0 = cb0_[c] * m, c1 = cb1_[c] * m, W = c1 - c0;
+    dev_.wait(S_MAIN, ev_b_[par][c]);
+    int64_t ra[2], rb[2], nr = 0;
+    if (has_next && x0 >= c0 && x0 < c1) {
+      if (x0 > c0) { ra[nr] = c0; rb[nr] = x0; ++nr; }
+      if (c1 > x1) { ra[nr] = x1; rb[nr] = c1; ++nr; }
+    } else {
+      ra[0] = c0; rb[0] = c1; nr = 1;
+    }
+    if (rows > 0)
+      for (int64_t z = 0; z < nr; ++z) {
+        GemmExtra ex = prows;
+        ex.zc0 = pc0 - ra[z];  // the panel's own block columns enter as 0
+        ex.zc1 = pc1 - ra[z];
+        dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, rb[z] - ra[z], K, At_[par], rows,
+                  rb_chunk(par, c) + (ra[z] - c0) * (int64_t)esz(), W, elem(X_, ra[z]), npad, S_MAIN,
+                  ex);
+      }
+    dev_.record(ev_c_[c], S_MAIN);
   }
   dbg_sync();
 }
@@ -210,7 +402,6 @@ SolveStats Engine::solve() {
   GJ_REQUIRE(!solved_, "solve(): input panel already consumed; load the matrix again");
   SolveStats st;
   const int64_t m = L_.m, Nr = L_.Nr, rows = L_.rows, npad = L_.npad;
-  const int64_t C = (int64_t)cb0_.size();
 
   comm_.barrier(dev_);
   const double t_begin = now_s();
@@ -234,105 +425,23 @@ SolveStats Engine::solve() {
 
   st.pivots.assign(Nr, -1);
   double host_wait = 0;
+  bool ok = true;
 
-  // ---- prologue: step 0 selection and broadcast
-  if (rows > 0) dev_.extract_neg_t(opt_.dtype, Lt_[0], rows, X_, npad, rows, 0, m, S_MAIN);
+  // prologue: column 0, pivot searches of panel 0
+  if (rows > 0) dev_.extract_neg_t(opt_.dtype, At_[0], rows, X_, npad, rows, 0, m, S_MAIN);
   dev_.record(ev_L_, S_MAIN);
-  dev_.wait(S_SIDE, ev_L_);
-  select(0);
-  {
-    const double w0 = now_s();
-    dev_.sync_event(ev_sel_[0]);
-    host_wait += now_s() - w0;
+  ok = factor_panel(0, /*wait_main=*/false, st, host_wait);
+
+  for (int64_t u = 0; ok && u < npanels(); ++u) {
+    big_update(u);
+    if (u + 1 < npanels()) ok = factor_panel(u + 1, /*wait_main=*/true, st, host_wait);
   }
-  PivotResult r = piv_host_[0];
-  PivotResult piv[2];
-  piv[0] = r;
-  if (!r.found) {
+  if (!ok) {
     dev_.sync_all();
-    st.status = Status::Singular;
-    st.singular_step = 0;
+    st.host_wait_ms = host_wait * 1e3;
     st.seconds = now_s() - t_begin;
     solved_ = true;
     return st;
-  }
-  st.pivots[0] = r.phys;
-  if (r.owner == L_.k) st.bcast_bytes += double(m) * npad * esz();
-  post_select(0, r);
-  normalize_and_bcast(0, r, /*wait_main=*/false);
-
-  // ---- main loop
-  for (int64_t t = 0; t < Nr; ++t) {
-    const int cur = (int)(t & 1), nx = cur ^ 1;
-    const bool has_next = (t + 1 < Nr);
-    dev_.wait(S_MAIN, ev_adj_[cur]);
-    // Step t on every local row i:  X[i, :] += (-L_i) R_t, except
-    //   * block column t enters as 0:   X[i, t] = -L_i H            (no I + H cancellation)
-    //   * the pivot rows s_t are overwritten with R_t (owner only).
-    const int64_t pr0 = (piv[cur].owner == L_.k) ? (piv[cur].phys / L_.p) * m : -1;
-    const int64_t tz0 = t * m, tz1 = tz0 + m;
-
-    if (has_next) {
-      // (a) look-ahead column block t+1 first
-      const int64_t b = t + 1, cb = chunk_of_[b];
-      const int64_t c0 = cb0_[cb] * m, W = (cb1_[cb] - cb0_[cb]) * m;
-      dev_.wait(S_MAIN, ev_b_[cur][cb]);
-      if (rows > 0) {
-        dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, m, m, Lt_[cur], rows,
-                  elem(R_[cur], m * c0 + (b * m - c0)), W, elem(X_, b * m), npad, S_MAIN, 0, 0, pr0);
-        dev_.extract_neg_t(opt_.dtype, Lt_[nx], rows, X_, npad, rows, b * m, m, S_MAIN);
-      }
-      dev_.record(ev_L_, S_MAIN);
-      dbg_sync();
-      // (b) pivot search for step t+1 on the SIDE stream
-      dev_.wait(S_SIDE, ev_L_);
-      select(t + 1);
-    }
-
-    // (c) the rest of step t's update, chunk by chunk
-    const int64_t start = has_next ? chunk_of_[t + 1] : 0;
-    for (int64_t i = 0; i < C; ++i) {
-      const int64_t c = (start + i) % C;
-      const int64_t c0 = cb0_[c] * m, c1 = cb1_[c] * m, W = c1 - c0;
-      dev_.wait(S_MAIN, ev_b_[cur][c]);
-      int64_t ra[2], rb[2], nr = 0;
-      if (has_next && (t + 1) >= cb0_[c] && (t + 1) < cb1_[c]) {
-        const int64_t x0 = (t + 1) * m, x1 = x0 + m;
-        if (x0 > c0) { ra[nr] = c0; rb[nr] = x0; ++nr; }
-        if (c1 > x1) { ra[nr] = x1; rb[nr] = c1; ++nr; }
-      } else {
-        ra[0] = c0; rb[0] = c1; nr = 1;
-      }
-      if (rows > 0)
-        for (int64_t q = 0; q < nr; ++q)
-          dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, rb[q] - ra[q], m, Lt_[cur], rows,
-                    elem(R_[cur], m * c0 + (ra[q] - c0)), W, elem(X_, ra[q]), npad, S_MAIN,
-                    tz0 - ra[q], tz1 - ra[q], pr0);
-      dev_.record(ev_c_[c], S_MAIN);
-    }
-    dbg_sync();
-
-    if (has_next) {
-      // (d) wait (host) for the pivot of step t+1 — normally long finished behind (c)
-      const double w0 = now_s();
-      dev_.sync_event(ev_sel_[nx]);
-      host_wait += now_s() - w0;
-      r = piv_host_[nx];
-      piv[nx] = r;
-      if (!r.found) {
-        dev_.sync_all();
-        st.status = Status::Singular;
-        st.singular_step = t + 1;
-        st.host_wait_ms = host_wait * 1e3;
-        st.seconds = now_s() - t_begin;
-        solved_ = true;
-        return st;
-      }
-      st.pivots[t + 1] = r.phys;
-      if (r.owner == L_.k) st.bcast_bytes += double(m) * npad * esz();
-      post_select(t + 1, r);
-      normalize_and_bcast(t + 1, r, /*wait_main=*/true);
-    }
   }
 
   finalize(st.pivots);

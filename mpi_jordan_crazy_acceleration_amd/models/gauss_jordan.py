@@ -42,6 +42,7 @@ class GaussJordan:
     dtype: str = "fp64"
     comm: str = "auto"
     chunk_cols: int = 0
+    depth: int = 2
     eps: float = 1e-15
     sync_debug: bool = False
     residual: str = "always"
@@ -51,7 +52,8 @@ class GaussJordan:
     def _cfg(self, n: int) -> dict:
         dev = _default_device() if self.device == "auto" else self.device
         cfg = dict(n=int(n), m=int(self.block_size), ranks=int(self.ranks), device=dev,
-                   dtype=self.dtype, comm=self.comm, chunk_cols=int(self.chunk_cols), eps=float(self.eps),
+                   dtype=self.dtype, comm=self.comm, chunk_cols=int(self.chunk_cols), depth=int(self.depth),
+                   eps=float(self.eps),
                    sync_debug=bool(self.sync_debug), residual=self.residual,
                    host_threads=int(self.host_threads))
         cfg.update(self.extra)

@@ -37,16 +37,16 @@ def _p(t: torch.Tensor) -> int:
 
 
 def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, op: str = "acc", a_kmajor: bool = False,
-         zero_cols=(0, 0), pivot_row0: int = -1) -> torch.Tensor:
+         zero_cols=(0, 0), zero_rows=(), zero_row_height: int = 0) -> torch.Tensor:
     """C += A@B (op="acc") or C = A@B (op="store").  With a_kmajor, ``A`` is given as A^T (K x M).
 
-    Elimination extras (op="acc"): C columns in ``zero_cols`` enter as 0; rows
-    [pivot_row0, pivot_row0 + K) are overwritten with the rows of B."""
+    Elimination extras (op="acc"): C enters as 0 in the columns ``zero_cols`` = (c0, c1) and in the
+    row blocks [r, r + zero_row_height) for r in ``zero_rows`` (at most 4)."""
     assert A.dtype == B.dtype == C.dtype and A.stride(-1) == 1 and B.stride(-1) == 1 and C.stride(-1) == 1
     M, N = C.shape
     K = A.shape[0] if a_kmajor else A.shape[1]
     device_for(C).gemm(_DT[C.dtype], op, a_kmajor, M, N, K, _p(A), A.stride(0), _p(B), B.stride(0), _p(C), C.stride(0),
-                       int(zero_cols[0]), int(zero_cols[1]), int(pivot_row0))
+                       int(zero_cols[0]), int(zero_cols[1]), [int(r) for r in zero_rows], int(zero_row_height))
     return C
 
 

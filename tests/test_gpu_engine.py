@@ -10,8 +10,9 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("n,m", [(1000, 128), (517, 60), (64, 64), (300, 256), (10, 12), (40, 1)])
 @pytest.mark.parametrize("gen", ["random", "absdiff"])
-def test_engine_single_gpu_vs_numpy(native, n, m, gen):
-    eng = native.Engine(native.hip_device(0), native.self_comm(), n, m, "fp64")
+@pytest.mark.parametrize("depth", [1, 2, 3])
+def test_engine_single_gpu_vs_numpy(native, n, m, gen, depth):
+    eng = native.Engine(native.hip_device(0), native.self_comm(), n, m, "fp64", 0, 1e-15, False, depth)
     eng.generate(gen, 5)
     st = eng.solve()
     assert st["status"] == 0
@@ -25,12 +26,13 @@ def test_engine_single_gpu_vs_numpy(native, n, m, gen):
 
 
 @pytest.mark.parametrize("p", [2, 3, 4])
-def test_loopback_ranks_on_one_gpu(p):
+@pytest.mark.parametrize("depth", [1, 2])
+def test_loopback_ranks_on_one_gpu(p, depth):
     n, m = 700, 64
     A = generate_matrix(n, "random", 9)
     # permuted, diagonally weak matrix forces off-diagonal pivots (swaps)
     A = A[::-1].copy()
-    inv = gj.GaussJordan(block_size=m, ranks=p, device="gpu", comm="loopback").inverse(A)
+    inv = gj.GaussJordan(block_size=m, ranks=p, device="gpu", comm="loopback", depth=depth, chunk_cols=128).inverse(A)
     ref = np.linalg.inv(A)
     assert np.abs(inv - ref).max() / np.abs(ref).max() < 1e-8
 
@@ -72,7 +74,7 @@ def test_sync_debug_equals_async(native):
     n, m = 1536, 128
     outs = []
     for sd in (False, True):
-        eng = native.Engine(native.hip_device(0), native.self_comm(), n, m, "fp64", 256, 1e-15, sd)
+        eng = native.Engine(native.hip_device(0), native.self_comm(), n, m, "fp64", 256, 1e-15, sd, 2)
         eng.generate("random", 4)
         assert eng.solve()["status"] == 0
         outs.append(eng.download_local_rows())

@@ -119,19 +119,21 @@ def test_row_abs_max_and_residual():
 @pytest.mark.parametrize("variant", ["big", "narrow", "tall", "valu"])
 @pytest.mark.parametrize("M,N,K", [(256, 384, 128), (300, 200, 60), (1000, 130, 256)])
 def test_gemm_variants_elimination_extras(native, variant, M, N, K):
-    """All kernel variants: C += A B with a zero-column range and pivot rows overwritten by B."""
+    """All kernel variants: C += A B where C enters as 0 in a column range and in two row blocks."""
     native.set_gemm_variant(variant)
     try:
         A = _rand((M, K), torch.float64, 11)
         B = _rand((K, N), torch.float64, 12)
         C = _rand((M, N), torch.float64, 13)
-        z0, z1, pr0 = 17, 17 + K // 2, 70
-        ref = C.clone()
-        ref[:, z0:z1] = 0
-        ref = ref + A @ B
-        ref[pr0:pr0 + K] = B[: min(K, M - pr0)]
+        z0, z1, zr, zh = 17, 17 + K // 2, [70, 190], 45
+        Cin = C.clone()
+        Cin[:, z0:z1] = 0
+        for r in zr:
+            Cin[r:r + zh] = 0
+        ref = Cin + A @ B
         Cd = C.cuda()
-        ops.gemm(A.t().contiguous().cuda(), B.cuda(), Cd, op="acc", a_kmajor=True, zero_cols=(z0, z1), pivot_row0=pr0)
+        ops.gemm(A.t().contiguous().cuda(), B.cuda(), Cd, op="acc", a_kmajor=True, zero_cols=(z0, z1),
+                 zero_rows=zr, zero_row_height=zh)
         assert (Cd.cpu() - ref).abs().max().item() < 1e-12 * K
         Cs = torch.zeros(M, N, dtype=torch.float64).cuda()
         ops.gemm(A.t().contiguous().cuda(), B.cuda(), Cs, op="store", a_kmajor=True)

@@ -114,3 +114,41 @@ def test_solve_rhs():
     b = A @ x
     got = gj.solve(A, b, block_size=16, device="cpu")
     assert np.abs(got - x).max() < 1e-9
+
+
+@pytest.mark.parametrize("depth", [1, 2, 3, 4])
+@pytest.mark.parametrize("n,m,p", [(37, 5, 1), (37, 5, 3), (64, 8, 2), (10, 3, 4), (50, 7, 5), (12, 12, 2)])
+@pytest.mark.parametrize("kind", ["rand", "perm"])
+def test_depth_variants_match_numpy(depth, n, m, p, kind):
+    A = _mat(kind, n, seed=n + m + p)
+    inv = gj.GaussJordan(block_size=m, ranks=p, device="cpu", depth=depth, chunk_cols=2 * m).inverse(A)
+    ref = np.linalg.inv(A)
+    assert np.abs(inv - ref).max() / np.abs(ref).max() < 1e-10
+
+
+@pytest.mark.parametrize("depth", [1, 2, 4])
+def test_depth_absdiff_residual_matches_reference_band(depth):
+    rep = gj.run(512, 64, ranks=2, device="cpu", gen="absdiff", depth=depth)
+    assert rep["status"] == 0 and rep["residual"] < 5e-8
+
+
+def test_depth_pivots_identical():
+    A = _mat("perm", 64, 4)
+    p1 = gj.GaussJordan(block_size=4, ranks=3, device="cpu", depth=1).run(64, input=A)["stats"]["pivots"]
+    p3 = gj.GaussJordan(block_size=4, ranks=3, device="cpu", depth=3).run(64, input=A)["stats"]["pivots"]
+    assert p1 == p3
+
+
+def test_host_gemm_extras_match_torch():
+    import torch
+    from mpi_jordan_crazy_acceleration_amd import ops
+    g = torch.Generator().manual_seed(3)
+    A = torch.rand(90, 20, generator=g, dtype=torch.float64)
+    B = torch.rand(20, 70, generator=g, dtype=torch.float64)
+    C = torch.rand(90, 70, generator=g, dtype=torch.float64)
+    Cin = C.clone()
+    Cin[:, 5:25] = 0
+    Cin[30:40] = 0
+    ref = Cin + A @ B
+    ops.gemm(A.t().contiguous(), B, C, op="acc", a_kmajor=True, zero_cols=(5, 25), zero_rows=[30], zero_row_height=10)
+    assert (C - ref).abs().max().item() < 1e-12
