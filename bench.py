@@ -37,7 +37,7 @@ def main() -> int:
     ap.add_argument("--gen", default="random")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--chunk-cols", type=int, default=0)
-    ap.add_argument("--depth", type=int, default=2, help="elimination steps fused per trailing update")
+    ap.add_argument("--depth", type=int, default=4, help="elimination steps fused per trailing update")
     ap.add_argument("--no-residual", action="store_true")
     ap.add_argument("--force-rccl", action="store_true", help="use the RCCL communicator even at 1 rank")
     ap.add_argument("--gemm-variant", default=None, help="big | narrow | tall (kernel tile config)")

@@ -9,15 +9,20 @@
 //     3n^3 (it eliminates the full-width B = I part every step, main.cpp:1176-1193).
 //   * Rows are never swapped; the pivot of step t is tracked as a physical block row s_t and the
 //     result is permuted once at the end (finalize).  A row swap therefore costs nothing per step.
-//   * Step t is ONE rank-m update of every local row:  X += Lt^T * R_t  with
-//        Lt  = -X[:, block t]  (K-major multiplier panel; the owner of s_t adds I to its block),
-//        R_t = H * X[s_t, :]  with block t replaced by I + H,  H = inv(X[s_t, block t]).
-//     That folds normalisation, the pivot-row write-back and the pivot-column update into the same
-//     MFMA GEMM (no special rows or columns in the hot kernel).
-//   * Look-ahead: column block t+1 is updated first; the SIDE stream runs the pivot search for step
-//     t+1 (batched block inverses + RCCL all-gather of 32-B records + deterministic argmin) while the
-//     MAIN stream runs the rest of step t's update; the COMM stream normalises and broadcasts the
-//     next pivot row chunk by chunk as soon as each column chunk of step t is finished.
+//   * Step t eliminates block column t from every row with the multipliers L_i = -X[i, t] and the
+//     normalised pivot row R_t = H * X[s_t, :], H = inv(X[s_t, t]).  The exact (cancellation-free)
+//     sweep form is used: column t enters the update as 0 (so X[i,t] becomes L_i H), the pivot row
+//     enters as 0 with its multiplier row edited to "I" at its own position (so it becomes R_t).
+//   * Depth-d panels: d consecutive steps are fused into ONE trailing update
+//        X += [L_t0 .. L_t0+d-1] * [R_t0 ; .. ; R_t0+d-1]        (K = d*m, MFMA GEMM)
+//     The panel's own d columns and d pivot rows are produced by narrow side updates ("panel
+//     pieces", d*m x d*m) so that the big GEMM needs only zero-column / zero-row masks (GemmExtra)
+//     and no special rows inside the hot kernel.  d = 4 gives K = 512 at m = 128.
+//   * Look-ahead (three HIP streams): MAIN runs the big update of panel u; SIDE (high priority)
+//     first updates the next panel's columns, then runs its pivot searches (batched in-register
+//     block inverses + RCCL all-gather of 32-B PivotRec + deterministic argmin on device) and the
+//     narrow edits; COMM normalises the next panel's pivot rows and broadcasts them chunk by chunk
+//     (one event per chunk) so MAIN's next update can start on chunk 0 while chunk k is in flight.
 #pragma once
 
 #include <algorithm>
@@ -33,7 +38,7 @@ namespace gj {
 struct SolveOptions {
   DType dtype = DType::F64;
   int64_t chunk_cols = 0;   // pipelining granularity of the pivot-row broadcast (0 = auto)
-  int depth = 2;            // elimination steps fused per trailing update (K = depth*m), 1..4
+  int depth = 4;            // elimination steps fused per trailing update (K = depth*m), 1..4
   double eps = kDefaultEps;
   bool sync_debug = false;  // synchronise every stream after every phase (race screening)
   bool profile = false;     // per-phase timing (adds synchronisation)

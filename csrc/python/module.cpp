@@ -234,7 +234,7 @@ PYBIND11_MODULE(_C, mod) {
            }),
            py::arg("device"), py::arg("comm"), py::arg("n"), py::arg("m"), py::arg("dtype") = "fp64",
            py::arg("chunk_cols") = 0, py::arg("eps") = kDefaultEps, py::arg("sync_debug") = false,
-           py::arg("depth") = 2)
+           py::arg("depth") = 4)
       .def_property_readonly("layout",
                              [](PyEngine& e) {
                                const Layout& L = e.eng->layout();

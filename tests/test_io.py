@@ -1,0 +1,35 @@
+"""Matrix file reader: the scanf("%lf") accept set (reference read_matrix, main.cpp:209-282)."""
+import numpy as np
+import pytest
+
+
+def test_reader_accept_set(native, tmp_path):
+    f = tmp_path / "m.txt"
+    # hex floats, exponents, signs, tokens glued like "1.5-2" (scanf reads two numbers), tabs/newlines
+    f.write_text("0x1p3 -2.5e0\t+3\n1.5-2   inf\n nan 7 8 9 trailing junk")
+    A = native.read_matrix_file(str(f), 3)
+    assert A[0, 0] == 8.0 and A[0, 1] == -2.5 and A[0, 2] == 3.0
+    assert A[1, 0] == 1.5 and A[1, 1] == -2.0 and np.isinf(A[1, 2])
+    assert np.isnan(A[2, 0]) and A[2, 1] == 7 and A[2, 2] == 8
+
+
+def test_reader_errors(native, tmp_path):
+    with pytest.raises(RuntimeError, match="cannot open"):
+        native.read_matrix_file(str(tmp_path / "missing.txt"), 2)
+    f = tmp_path / "bad.txt"
+    f.write_text("1 2 x 4")
+    with pytest.raises(RuntimeError, match="cannot read"):
+        native.read_matrix_file(str(f), 2)
+    g = tmp_path / "ok_after.txt"
+    g.write_text("1 2 3 4 x")  # junk after the first n*n numbers is ignored
+    assert native.read_matrix_file(str(g), 2).tolist() == [[1, 2], [3, 4]]
+
+
+def test_reader_parallel_large(native, tmp_path):
+    n = 400  # > 1 MiB of text -> multi-threaded chunked parse
+    A = np.random.default_rng(0).standard_normal((n, n)) * 1e5
+    f = tmp_path / "big.txt"
+    np.savetxt(f, A, fmt="%.17g")
+    assert f.stat().st_size > (1 << 20)
+    B = native.read_matrix_file(str(f), n)
+    assert np.array_equal(A, B)
