@@ -5,7 +5,9 @@
 // candidate block of the current block column at main.cpp:1039-1066.
 //
 // One workgroup per candidate block.  The m x m block (padded to MP = 32/64/128/256) lives in
-// REGISTERS: thread (tr, tc) owns rows i = tc + 32*qi and columns j = tr + TR*cj, so the global load
+// REGISTERS (16 elements per thread for MP = 64/128, measured 4x faster per step than 64 elements
+// per thread at one wave per SIMD): thread (tr, tc) owns rows i = tc + 32*qi and columns
+// j = tr + TR*cj, so the global load
 // from the K-major multiplier panel is coalesced along i.  Each of the m elimination steps needs two
 // workgroup barriers: column k is published to LDS, every wave redundantly computes the pivot argmax
 // (no third barrier), the pivot-row owners publish the scaled pivot row, then every thread applies
@@ -21,6 +23,48 @@
 
 namespace gj {
 namespace kern {
+
+// ---- wave-wide max of a double without LDS round trips: DPP quad/row permutes for the first
+// 16 lanes, v_permlane16_swap / v_permlane32_swap (gfx950) for the rest.
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double x) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, x);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ double join64(unsigned lo, unsigned hi) {
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double wave_max_f64(double v) {
+  v = fmax(v, dpp64<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = fmax(v, dpp64<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = fmax(v, dpp64<0x141>(v));  // row_half_mirror (8)
+  v = fmax(v, dpp64<0x140>(v));  // row_mirror (16)
+  {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const auto l = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+    v = fmax(join64(l[0], h[0]), join64(l[1], h[1]));
+  }
+  {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const auto l = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+    v = fmax(join64(l[0], h[0]), join64(l[1], h[1]));
+  }
+  return v;
+}
+// Pivot key: |a| with its lowest 8 mantissa bits replaced by (255 - row), so one wave-wide double
+// max yields the largest magnitude and, among (near-)equal magnitudes, the lowest row.
+__device__ __forceinline__ double pivot_key(double a, int row) {
+  if (!(a == a)) a = 0.0;
+  const uint64_t b = (__builtin_bit_cast(uint64_t, a) & ~uint64_t(0xFF)) | (uint64_t)(255 - row);
+  return __builtin_bit_cast(double, b);
+}
+__device__ __forceinline__ int pivot_key_row(double key) {
+  return 255 - (int)(__builtin_bit_cast(uint64_t, key) & 0xFF);
+}
 
 template <typename T, int MP, int NTH>
 __global__ __launch_bounds__(NTH) void block_inverse_kernel(const T* __restrict__ Lt, int64_t ldl,
@@ -75,8 +119,9 @@ __global__ __launch_bounds__(NTH) void block_inverse_kernel(const T* __restrict_
   for (int kk = 0; kk < m; ++kk) {
     const int par = kk & 1;
     const int kcj = kk / TR;
-    // (1) publish column kk
-    if (tr == kk % TR) {
+    const bool col_owner = (tr == kk % TR);
+    // (1) publish column kk (one half-wave owns it)
+    if (col_owner) {
 #pragma unroll
       for (int qi = 0; qi < RI; ++qi) {
         T v = T(0);
@@ -87,34 +132,22 @@ __global__ __launch_bounds__(NTH) void block_inverse_kernel(const T* __restrict_
       }
     }
     __syncthreads();
-    // (2) argmax |colv| over unused real rows, lowest index on ties (every wave, redundantly)
-    double best = -1.0;
-    int bi = MP;
+    // (2) argmax |colv| over unused real rows, lowest row on ties (every wave, redundantly, with
+    // register-only cross-lane moves); r is wave-uniform -> scalar branches below
+    double key = -1.0;
 #pragma unroll
     for (int s = 0; s < SCAN; ++s) {
       const int i = lane + 64 * s;
-      if (i < m && !lused[s]) {
-        const double v = fabs((double)colv[par][i]);
-        if (v > best) {
-          best = v;
-          bi = i;
-        }
-      }
+      const double kv = (i < m && !lused[s]) ? pivot_key(fabs((double)colv[par][i]), i) : -1.0;
+      key = fmax(key, kv);
     }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      const double ob = __shfl_xor(best, off, 64);
-      const int oi = __shfl_xor(bi, off, 64);
-      if (ob > best || (ob == best && oi < bi)) {
-        best = ob;
-        bi = oi;
-      }
-    }
-    if (!(best >= thresh)) {  // uniform across the workgroup (same data, same reduction order)
+    key = wave_max_f64(key);
+    const int r = __builtin_amdgcn_readfirstlane(pivot_key_row(key));
+    const T pivv = colv[par][r];
+    if (!(fabs((double)pivv) >= thresh)) {  // uniform across the workgroup
       singular = true;
       break;
     }
-    const int r = bi;
 #pragma unroll
     for (int s = 0; s < SCAN; ++s)
       if (lane + 64 * s == r) lused[s] = true;
@@ -122,37 +155,46 @@ __global__ __launch_bounds__(NTH) void block_inverse_kernel(const T* __restrict_
       prow[kk] = r;
       kinv[r] = kk;
     }
-    const T inv = T(1) / colv[par][r];
-    // (3) publish the scaled pivot row
-    if (tc == (r & 31)) {
-      const int rq = r >> 5;
+    const T inv = T(1) / pivv;
+    const int rq = r >> 5;
+    const bool row_owner = (tc == (r & 31));
+    // (3) publish the scaled pivot row (rowv[kk] = inv)
+    if (row_owner) {
 #pragma unroll
-      for (int cj = 0; cj < CJ; ++cj) {
-        T v = T(0);
+      for (int qi = 0; qi < RI; ++qi)
+        if (qi == rq) {
 #pragma unroll
-        for (int qi = 0; qi < RI; ++qi)
-          if (qi == rq) v = w[qi][cj];
-        const int j = tr + TR * cj;
-        rowv[par][j] = (j == kk) ? inv : v * inv;
-      }
+          for (int cj = 0; cj < CJ; ++cj) {
+            const int j = tr + TR * cj;
+            rowv[par][j] = (j == kk) ? inv : w[qi][cj] * inv;
+          }
+        }
     }
     __syncthreads();
-    // (4) rank-1 update
+    // (4) rank-1 update: column kk enters as 0 (-> -f*inv), pivot row fixed up afterwards
+    if (col_owner) {
+#pragma unroll
+      for (int qi = 0; qi < RI; ++qi)
+#pragma unroll
+        for (int cj = 0; cj < CJ; ++cj)
+          if (cj == kcj) w[qi][cj] = T(0);
+    }
+    T rv[CJ];
+#pragma unroll
+    for (int cj = 0; cj < CJ; ++cj) rv[cj] = rowv[par][tr + TR * cj];
 #pragma unroll
     for (int qi = 0; qi < RI; ++qi) {
-      const int i = tc + 32 * qi;
-      const T f = colv[par][i];
+      const T nf = -colv[par][tc + 32 * qi];
 #pragma unroll
-      for (int cj = 0; cj < CJ; ++cj) {
-        const int j = tr + TR * cj;
-        const T rv = rowv[par][j];
-        if (i == r) {
-          w[qi][cj] = rv;
-        } else {
-          const T old = (j == kk) ? T(0) : w[qi][cj];
-          w[qi][cj] = old - f * rv;
+      for (int cj = 0; cj < CJ; ++cj) w[qi][cj] = __builtin_fma(nf, rv[cj], w[qi][cj]);
+    }
+    if (row_owner) {
+#pragma unroll
+      for (int qi = 0; qi < RI; ++qi)
+        if (qi == rq) {
+#pragma unroll
+          for (int cj = 0; cj < CJ; ++cj) w[qi][cj] = rv[cj];
         }
-      }
     }
   }
 
@@ -337,9 +379,9 @@ static void launch_bi(const void* Lt, int64_t ldl, void* inv_t, double* scores, 
   else if (m <= 64)
     hipLaunchKernelGGL((block_inverse_kernel<T, 64, 256>), dim3(grid), dim3(256), 0, s, lt, ldl, it,
                        scores, valid, used, m, L.p, L.k, thresh);
-  else if (m <= 128)
-    hipLaunchKernelGGL((block_inverse_kernel<T, 128, 256>), dim3(grid), dim3(256), 0, s, lt, ldl, it,
-                       scores, valid, used, m, L.p, L.k, thresh);
+  else if (m <= 128)  // 16 elements per thread, 4 waves per SIMD to hide the per-step latency chain
+    hipLaunchKernelGGL((block_inverse_kernel<T, 128, 1024>), dim3(grid), dim3(1024), 0, s, lt, ldl,
+                       it, scores, valid, used, m, L.p, L.k, thresh);
   else if (m <= 256 && sizeof(T) == 4)  // 256x256 fp32 = 64 VGPRs/lane at 1024 threads
     hipLaunchKernelGGL((block_inverse_kernel<T, 256, 1024>), dim3(grid), dim3(1024), 0, s, lt, ldl,
                        it, scores, valid, used, m, L.p, L.k, thresh);
