@@ -1,5 +1,8 @@
 #!/usr/bin/env python3
-"""Latency of the batched candidate-block inversion (pivot search) in isolation."""
+"""Latency of the batched candidate-block inversion (pivot search) in isolation.
+
+    python bench/bench_blockinv.py [panel] [sweep]
+"""
 import json
 import os
 import sys
@@ -8,20 +11,30 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-from mpi_jordan_crazy_acceleration_amd import ops  # noqa: E402
+from mpi_jordan_crazy_acceleration_amd import load_native, ops  # noqa: E402
 
-for m in (64, 128):
-    for nblk in (8, 32, 256):
-        for dt in (torch.float64, torch.float32):
-            Lt = torch.randn(m, nblk * m, dtype=dt, device="cuda")
-            n = nblk * m
-            ops.block_inverse(Lt, n, m)
-            torch.cuda.synchronize()
-            reps = 20
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                ops.block_inverse(Lt, n, m)
-            torch.cuda.synchronize()
-            us = (time.perf_counter() - t0) / reps * 1e6
-            print(json.dumps({"m": m, "nblk": nblk, "dtype": str(dt).split(".")[-1], "us_per_call": round(us, 1),
-                              "us_per_step": round(us / m, 3)}), flush=True)
+
+def main(variants):
+    C = load_native()
+    for var in variants:
+        C.set_block_inverse_variant(var)
+        for m in (64, 128):
+            for nblk in (8, 32, 256):
+                for dt in (torch.float64, torch.float32):
+                    Lt = torch.randn(m, nblk * m, dtype=dt, device="cuda")
+                    n = nblk * m
+                    ops.block_inverse(Lt, n, m)
+                    torch.cuda.synchronize()
+                    reps = 20
+                    t0 = time.perf_counter()
+                    for _ in range(reps):
+                        ops.block_inverse(Lt, n, m)
+                    torch.cuda.synchronize()
+                    us = (time.perf_counter() - t0) / reps * 1e6
+                    print(json.dumps({"variant": var, "m": m, "nblk": nblk, "dtype": str(dt).split(".")[-1],
+                                      "us_per_call": round(us, 1), "us_per_step": round(us / m, 3)}), flush=True)
+    C.set_block_inverse_variant("panel")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:] or ["panel", "sweep"])

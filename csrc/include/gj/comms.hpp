@@ -86,3 +86,35 @@ class LoopbackComm : public Comm {
 };
 
 }  // namespace gj
+
+namespace gj {
+
+// ---------------------------------------------------------------- critical-path emulation
+// Rank 0 of a p-rank job, alone on one device: lets a 1-GPU box time the per-rank critical path
+// of a p-GPU solve (1/p of the rows, every step's pivot search / panel pieces / chunk pipeline,
+// the full-width trailing update) without p GPUs.  Peers are synthetic: at step t the pivot is
+// rank 0's own best candidate when t % p == 0, otherwise block row t (owned by rank t % p) with
+// a winning score; rows "received" from peers are zeros.  The inverse is meaningless; only the
+// timing is.  Communication time itself is NOT emulated (broadcasts are local memsets).
+class ShadowComm : public Comm {
+ public:
+  explicit ShadowComm(int p) : p_(p) {}
+  int size() const override { return p_; }
+  int rank() const override { return 0; }
+  std::string describe() const override { return "shadow(" + std::to_string(p_) + ")"; }
+  void allgather(Device& dev, const void* send, void* recv, size_t bytes, int s) override;
+  void bcast(Device& dev, void* buf, size_t bytes, int root, int s) override;
+  void allreduce_max(Device&, double*, size_t, int) override {}
+  void group_p2p(Device&, const std::vector<P2POp>&, int) override {}
+  void barrier(Device& dev) override { dev.sync_all(); }
+  double host_max(Device&, double v) override { return v; }
+  void host_allgather(Device& dev, const void* send, void* recv, size_t bytes) override;
+  void reset() { step_ = 0; }
+
+ private:
+  int p_;
+  int64_t step_ = 0;
+  std::vector<char> host_;
+};
+
+}  // namespace gj

@@ -21,6 +21,8 @@ void gemm_valu(int op, int64_t M, int64_t N, int64_t K, const void* At, int64_t 
                int64_t ldb, void* C, int64_t ldc, hipStream_t s, const GemmExtra* ex);
 int gemm_variant_id(const char* name);  // big | narrow | tall | valu
 void set_gemm_variant(int v);
+void set_block_inverse_variant(int v);  // 0 = panel-blocked (default), 1 = per-step sweep
+int block_inverse_variant();
 void residual_partial(DType dt, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                       const void* B, int64_t ldb, int64_t n_real, int64_t blk_m, int64_t p,
                       int64_t k, double* partial, hipStream_t s);

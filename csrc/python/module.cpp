@@ -118,6 +118,11 @@ PYBIND11_MODULE(_C, mod) {
     return n;
   });
   mod.def("rccl_unique_id", [] { return py::bytes(RcclComm::unique_id()); });
+  mod.def("set_block_inverse_variant", [](const std::string& v) {
+    if (v == "panel") kern::set_block_inverse_variant(0);
+    else if (v == "sweep") kern::set_block_inverse_variant(1);
+    else throw std::invalid_argument("block inverse variant: panel | sweep");
+  });
   mod.def("set_gemm_variant", [](const std::string& v) { kern::set_gemm_variant(kern::gemm_variant_id(v.c_str())); });
 
   // Kernel-level entry points (raw pointers; used by the per-kernel numerics tests and
@@ -206,6 +211,13 @@ PYBIND11_MODULE(_C, mod) {
             py::gil_scoped_release rel;
             return std::shared_ptr<Comm>(new RcclComm(s, nranks, rank, device));
           });
+  mod.def("shadow_comm", [](int p) { return std::shared_ptr<Comm>(new ShadowComm(p)); },
+          "rank 0 of a p-rank job alone on one device (critical-path timing emulation)");
+  mod.def("shadow_reset", [](std::shared_ptr<Comm> c) {
+    auto* sc = dynamic_cast<ShadowComm*>(c.get());
+    GJ_REQUIRE(sc != nullptr, "shadow_reset: not a shadow communicator");
+    sc->reset();
+  });
   mod.def("py_comm", [](py::object impl, int rank, int size) {
     return std::shared_ptr<Comm>(new PyComm(std::move(impl), rank, size));
   });

@@ -59,15 +59,23 @@ def test_extract_neg_t():
     assert torch.equal(Lt.cpu(), -X.cpu()[:, 128:224].t())
 
 
-@pytest.mark.parametrize("m", [16, 60, 128, 200, 256, 300])
+@pytest.fixture(params=["panel", "sweep"])
+def bi_variant(request, native):
+    native.set_block_inverse_variant(request.param)
+    yield request.param
+    native.set_block_inverse_variant("panel")
+
+
+@pytest.mark.parametrize("m", [16, 37, 60, 64, 100, 128, 200, 256, 300])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
-def test_block_inverse(m, dtype):
-    nblk = 5
+def test_block_inverse(m, dtype, bi_variant):
+    nblk = 6
     rows = nblk * m
     rng = np.random.default_rng(m)
     W = rng.standard_normal((nblk, m, m)) + 0.0
     W[2] = 0.0  # singular candidate
     W[3] = np.eye(m) * 2.0  # exact inverse 0.5 I
+    W[5][:, m // 2] = 0.0  # exactly singular part-way through the sweep
     X = np.zeros((rows, m))
     for b in range(nblk):
         X[b * m:(b + 1) * m] = W[b]
@@ -75,7 +83,7 @@ def test_block_inverse(m, dtype):
     n = rows
     inv_t, scores, valid = ops.block_inverse(Lt, n, m, 1, 0, thresh=1e-12)
     valid = valid.cpu().numpy()
-    assert list(valid) == [1, 1, 0, 1, 1]
+    assert list(valid) == [1, 1, 0, 1, 1, 0]
     tol = 1e-8 if dtype == torch.float64 else 2e-2
     for b in [0, 1, 3, 4]:
         ref = np.linalg.inv(W[b].astype(np.float32 if dtype == torch.float32 else np.float64).astype(np.float64))
