@@ -17,7 +17,7 @@ CXXSTD    := -std=c++17
 COMMON    := -O3 -fPIC $(CXXSTD) -Icsrc/include -Wall -Wno-unused-result
 HIPFLAGS  := $(COMMON) --offload-arch=$(ARCH) -mcode-object-version=5 -munsafe-fp-atomics
 HOSTFLAGS := $(COMMON) -x c++ -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
-LDLIBS    := -L$(ROCM)/lib -lrccl -lamdhip64 -lpthread
+LDLIBS    := -L$(ROCM)/lib -lrccl -lamdhip64 -lrocprofiler-sdk-roctx -lpthread
 
 KERNELS   := gemm gemm_valu blockinv misc
 HOST_SRC  := solver/engine solver/runner runtime/host_device runtime/hip_device \

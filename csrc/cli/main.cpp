@@ -25,8 +25,12 @@
 //   --depth D            elimination steps fused per trailing update (1..4, default 4)
 //   --repeat R           time R solves, report the last (min also in --json)
 //   --out FILE           write the inverse (text, or .bin)
+//   --rhs ones|random|FILE  also solve A x = b (x = inv(A) b) and report ||A x - b||_inf
+//   --out-x FILE         write x (text, or .bin); implies --rhs ones unless --rhs is given
 //   --json               machine-readable report on stderr
 //   --sync-debug         synchronise after every phase (race screening)
+//   --profile            per-phase device timers (in --json) + roctx ranges for rocprofv3
+//   --comm-timeout S     seconds a rank waits for a pivot before declaring a peer failure
 //   --wait-debugger S    sleep S seconds at start (reference -DSLEEP, main.cpp:8, :70-72)
 #include <hip/hip_runtime.h>
 #include <unistd.h>
@@ -49,23 +53,40 @@ static int usage(const char* prog) {
 }
 
 static void json_report(const RunConfig& cfg, const RunReport& rep) {
+  std::string phases;
+  if (rep.stats.profiled) {
+    phases = ", \"phases_ms\": {";
+    for (int i = 0; i < kNumPhases; ++i) {
+      char buf[96];
+      std::snprintf(buf, sizeof buf, "%s\"%s\": %.3f", i ? ", " : "", phase_name(i), rep.stats.phase_ms[i]);
+      phases += buf;
+    }
+    phases += "}";
+  }
+  std::string rhs;
+  if (rep.rhs_solved) {
+    char buf[128];
+    std::snprintf(buf, sizeof buf, ", \"axb_residual\": %.6e, \"axb_seconds\": %.6f", rep.rhs_residual,
+                  rep.rhs_seconds);
+    rhs = buf;
+  }
   std::fprintf(stderr,
                "{\"n\": %lld, \"m\": %lld, \"ranks\": %d, \"device\": \"%s\", \"comm\": \"%s\", "
                "\"dtype\": \"%s\", \"status\": %d, \"glob_time\": %.6f, \"best_time\": %.6f, "
                "\"gflops_nominal\": %.3f, \"residual\": %.6e, \"residual_computed\": %s, "
-               "\"host_wait_ms\": %.3f, \"offdiag_pivots\": %lld}\n",
+               "\"host_wait_ms\": %.3f, \"offdiag_pivots\": %lld%s%s}\n",
                (long long)cfg.n, (long long)cfg.m, cfg.ranks, rep.device_desc.c_str(),
                rep.comm_desc.c_str(), dtype_name(cfg.solve.dtype), (int)rep.status, rep.glob_time,
                rep.best_time, rep.gflops_nominal, rep.residual,
                rep.residual_computed ? "true" : "false", rep.stats.host_wait_ms,
-               (long long)rep.stats.offdiag_pivots);
+               (long long)rep.stats.offdiag_pivots, phases.c_str(), rhs.c_str());
 }
 
 int main(int argc, char* argv[]) {
   RunConfig cfg;
   std::vector<const char*> pos;
   bool json = false;
-  std::string device = "auto", out_file;
+  std::string device = "auto", out_file, x_file;
   int wait_dbg = 0;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
@@ -105,8 +126,12 @@ int main(int argc, char* argv[]) {
       else if (a == "--depth") cfg.solve.depth = std::atoi(val("--depth"));
       else if (a == "--repeat") cfg.repeats = std::atoi(val("--repeat"));
       else if (a == "--out") out_file = val("--out");
+      else if (a == "--rhs") cfg.rhs = val("--rhs");
+      else if (a == "--out-x") x_file = val("--out-x");
       else if (a == "--json") json = true;
       else if (a == "--sync-debug") cfg.solve.sync_debug = true;
+      else if (a == "--profile") cfg.solve.profile = true;
+      else if (a == "--comm-timeout") cfg.solve.comm_timeout_s = std::atof(val("--comm-timeout"));
       else if (a == "--wait-debugger") wait_dbg = std::atoi(val("--wait-debugger"));
       else if (a == "--host-threads") cfg.host_threads = std::atoi(val("--host-threads"));
       else if (a == "--first-device") cfg.first_device = std::atoi(val("--first-device"));
@@ -135,6 +160,8 @@ int main(int argc, char* argv[]) {
     return usage(argv[0]);
   }
   cfg.keep_inverse = !out_file.empty();
+  cfg.keep_solution = !x_file.empty();
+  if (!x_file.empty() && cfg.rhs.empty()) cfg.rhs = "ones";
 
   RunReport rep;
   try {
@@ -146,8 +173,8 @@ int main(int argc, char* argv[]) {
   // error reporting mirrors main.cpp:372-449
   switch (rep.status) {
     case Status::Ok: break;
-    case Status::CannotOpen: std::printf("cannot open %s\n", cfg.file.c_str()); return 2;
-    case Status::CannotRead: std::printf("cannot read %s\n", cfg.file.c_str()); return 2;
+    case Status::CannotOpen: std::printf("%s\n", rep.message.c_str()); return 2;
+    case Status::CannotRead: std::printf("%s\n", rep.message.c_str()); return 2;
     case Status::NoMemory: std::printf("Not enough memory!\n"); if (!rep.message.empty()) std::fprintf(stderr, "%s\n", rep.message.c_str()); return 2;
     case Status::Singular:
       std::printf("A\n");
@@ -166,7 +193,13 @@ int main(int argc, char* argv[]) {
     std::printf("residual: %e\n", rep.residual);
   else if (cfg.residual == ResidualMode::Compat)
     std::printf("p == 1!\n");
+  if (rep.rhs_solved) {  // only with --rhs: the reference has no A x = b mode
+    std::printf("solution x:\n");
+    for (double v : rep.x_head) std::printf("%.2f\t", v);
+    std::printf("\nAx-b residual: %e\n", rep.rhs_residual);
+  }
   if (!out_file.empty()) write_matrix_file(out_file, n, rep.inverse.data(), n);
+  if (!x_file.empty()) write_vector_file(x_file, n, rep.x.data());
   if (json) json_report(cfg, rep);
   return 0;
 }

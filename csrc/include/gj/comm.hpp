@@ -42,6 +42,12 @@ class Comm {
   virtual void barrier(Device& dev) = 0;
   virtual double host_max(Device& dev, double v) = 0;
   virtual void host_allgather(Device& dev, const void* send, void* recv, size_t bytes) = 0;
+
+  // Failure detection: throw Error(CommError) if the transport reports an
+  // asynchronous failure (a peer died, a link error); abort() tears the transport down so that
+  // device-side collectives blocked on a dead peer return.
+  virtual void check_health() {}
+  virtual void abort() {}
 };
 
 // A trivial single-rank communicator.

@@ -33,6 +33,8 @@ class RcclComm : public Comm {
   void barrier(Device& dev) override;
   double host_max(Device& dev, double v) override;
   void host_allgather(Device& dev, const void* send, void* recv, size_t bytes) override;
+  void check_health() override;
+  void abort() override;
 
  private:
   void* comm_for(int s) const;

@@ -66,6 +66,7 @@ class Device {
   virtual void record(int ev, int s) = 0;
   virtual void wait(int s, int ev) = 0;
   virtual void sync_event(int ev) = 0;
+  virtual bool query_event(int ev) = 0;  // true once all work before the record has completed
   virtual void sync_stream(int s) = 0;
   virtual void sync_all() = 0;
   virtual float event_ms(int ev_start, int ev_end) = 0;

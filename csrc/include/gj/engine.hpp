@@ -41,13 +41,24 @@ struct SolveOptions {
   int depth = 4;            // elimination steps fused per trailing update (K = depth*m), 1..4
   double eps = kDefaultEps;
   bool sync_debug = false;  // synchronise every stream after every phase (race screening)
-  bool profile = false;     // per-phase timing (adds synchronisation)
+  bool profile = false;     // per-phase device timers (HIP events) + roctx ranges
+  double comm_timeout_s = 600;  // a host wait on a pivot longer than this is a peer failure
 };
 
-struct PhaseTimes {
-  double select_ms = 0;     // pivot search + exchange (host-visible wait)
-  double total_ms = 0;
+// Device time per phase (sum over the solve; phases on different streams overlap in time).
+enum Phase : int {
+  PH_COLUMN = 0,   // SIDE: next pivot column brought up to date + transposed multipliers
+  PH_PIVOT,        // SIDE: batched candidate inverses + local argmin
+  PH_EXCHANGE,     // SIDE: pivot record all-gather + global argmin + 32-B readback
+  PH_EDITS,        // SIDE: owner-side multiplier / H edits
+  PH_PIECES,       // COMM: panel pieces (owner GEMMs) + their broadcast
+  PH_NORMALISE,    // COMM: owner normalises its pivot rows chunk by chunk (GEMM)
+  PH_BCAST,        // COMM: pivot-row chunk broadcasts
+  PH_UPDATE,       // MAIN: depth-d trailing update (the MFMA GEMM)
+  PH_FINALIZE,     // COMM: final block permutation + exchange
+  kNumPhases
 };
+const char* phase_name(int ph);
 
 struct SolveStats {
   Status status = Status::Ok;
@@ -57,6 +68,9 @@ struct SolveStats {
   std::vector<int32_t> pivots;   // physical pivot block row of every step
   int64_t offdiag_pivots = 0;    // steps whose pivot was not the "natural" row (needed a swap)
   double bcast_bytes = 0;        // bytes of pivot rows broadcast by this rank (as root)
+  bool profiled = false;
+  double phase_ms[kNumPhases] = {};   // SolveOptions::profile only
+  int64_t phase_calls[kNumPhases] = {};
 };
 
 class Engine {
@@ -91,6 +105,13 @@ class Engine {
   double residual_generated(GenSpec g);
   double residual_rows(const double* host, int64_t ld);
 
+  // ---- A x = b (BASELINE config 1; SURVEY.md §5.6 --rhs) ----
+  // x = inv(A) b from the result panel: one MFMA GEMV per rank + all-gather (collective).
+  // b and x are full n-vectors on every rank.
+  void apply_inverse(const double* b, double* x);
+  // ||A x - b||_inf with the input panel currently holding A (after generate/upload; collective).
+  double axb_residual(const double* x, const double* b);
+
   int64_t real_local_rows() const;
 
  private:
@@ -107,6 +128,13 @@ class Engine {
   void finalize(const std::vector<int32_t>& seq);
   double residual_common();
   void dbg_sync();
+  // Host wait for a pivot result with failure detection (Comm::check_health + timeout).
+  void wait_pivot(int ev, int64_t step, double& host_wait);
+  // profiling: begin() records a timing event on stream s, end() closes the interval
+  int prof_begin(int s);
+  void prof_end(int phase, int ev0, int s);
+  int prof_event();
+  void prof_collect(SolveStats& st);
   size_t esz() const { return dtype_size(opt_.dtype); }
   char* elem(void* base, int64_t off) const { return static_cast<char*>(base) + off * (int64_t)esz(); }
   int64_t panel_t0(int64_t v) const { return v * d_; }
@@ -164,6 +192,10 @@ class Engine {
   int ev_pp_[2][kMaxDepth] = {};
   std::vector<int> ev_c_;        // per chunk: MAIN finished the panel update of that chunk
   std::vector<int> ev_b_[2];     // per chunk: all stacked rows of that chunk broadcast
+  std::vector<int> pev_pool_;    // profiling events (timing enabled), reused across solves
+  size_t pev_next_ = 0;
+  struct PMark { int phase, ev0, ev1; };
+  std::vector<PMark> pmarks_;
   bool solved_ = false;
 };
 

@@ -30,6 +30,7 @@ class HipDevice : public Device {
   void record(int ev, int s) override;
   void wait(int s, int ev) override;
   void sync_event(int ev) override;
+  bool query_event(int ev) override;
   void sync_stream(int s) override;
   void sync_all() override;
   float event_ms(int ev_start, int ev_end) override;

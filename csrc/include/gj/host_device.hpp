@@ -1,6 +1,8 @@
 // HostDevice — synchronous C++ reference executor (see host_device.cpp).
 #pragma once
 
+#include <vector>
+
 #include "gj/device.hpp"
 
 namespace gj {
@@ -26,6 +28,7 @@ class HostDevice : public Device {
   void record(int ev, int s) override;
   void wait(int s, int ev) override;
   void sync_event(int ev) override;
+  bool query_event(int) override { return true; }
   void sync_stream(int s) override;
   void sync_all() override;
   float event_ms(int ev_start, int ev_end) override;
@@ -59,6 +62,7 @@ class HostDevice : public Device {
  private:
   int nthreads_ = 1;
   int nev_ = 0;
+  std::vector<double> ev_time_;  // host ms at record()
 };
 
 }  // namespace gj

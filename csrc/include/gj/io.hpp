@@ -17,9 +17,14 @@ namespace gj {
 // accept set as scanf("%lf").  Files ending in ".bin" are raw little-endian fp64 (n*n values).
 // Returns Ok, CannotOpen or CannotRead.  Parsing is parallel (nthreads, 0 = auto).
 Status read_matrix_file(const std::string& path, int64_t n, std::vector<double>& out, int nthreads = 0);
+// Same parser for the first `count` numbers (right-hand sides: count = n).
+Status read_values_file(const std::string& path, size_t count, std::vector<double>& out, int nthreads = 0);
 
 // Writes an n x n fp64 matrix as text ("%.17g", one row per line) or raw binary (".bin").
 Status write_matrix_file(const std::string& path, int64_t n, const double* a, int64_t ld);
+
+// n values, one per line ("%.17g") or raw fp64 (".bin").
+Status write_vector_file(const std::string& path, int64_t n, const double* x);
 
 // print_row semantics: nm rows of nm values, "%.*f\t" each, newline per row.
 void print_corner(FILE* f, const std::vector<double>& corner, int nm, int precision = 2);

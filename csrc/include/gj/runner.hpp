@@ -28,6 +28,11 @@ struct RunConfig {
   bool keep_inverse = false;        // gather the full inverse into RunReport::inverse
   int host_threads = 0;
   int repeats = 1;                  // timed solves (the last one is reported; min kept too)
+  // A x = b after the inversion: "" (off), "ones", "random" (seeded by gen.seed), or a file of n
+  // numbers (text / .bin).  x = inv(A) b, then ||A x - b||_inf.
+  std::string rhs;
+  const double* rhs_input = nullptr;  // or a caller-owned n-vector
+  bool keep_solution = false;         // return x in RunReport::x
 };
 
 struct RunReport {
@@ -43,6 +48,11 @@ struct RunReport {
   SolveStats stats;                 // rank 0
   std::string device_desc, comm_desc;
   double gflops_nominal = 0;        // 2 n^3 / glob_time / 1e9
+  bool rhs_solved = false;
+  double rhs_residual = 0;          // ||A x - b||_inf
+  double rhs_seconds = 0;           // x = inv(A) b (GEMV + all-gather), max over ranks
+  std::vector<double> x_head;       // first min(n, print_max) entries of x
+  std::vector<double> x;            // n entries if keep_solution
 };
 
 RunReport run_local(const RunConfig& cfg);

@@ -43,7 +43,10 @@ size_t parse_range(const char* b, const char* e, std::vector<double>& out, size_
 }  // namespace
 
 Status read_matrix_file(const std::string& path, int64_t n, std::vector<double>& out, int nthreads) {
-  const size_t need = (size_t)n * (size_t)n;
+  return read_values_file(path, (size_t)n * (size_t)n, out, nthreads);
+}
+
+Status read_values_file(const std::string& path, size_t need, std::vector<double>& out, int nthreads) {
   FILE* f = std::fopen(path.c_str(), "rb");
   if (!f) return Status::CannotOpen;
   if (ends_with(path, ".bin")) {
@@ -110,6 +113,17 @@ Status write_matrix_file(const std::string& path, int64_t n, const double* a, in
       std::fputc('\n', f);
     }
   }
+  std::fclose(f);
+  return Status::Ok;
+}
+
+Status write_vector_file(const std::string& path, int64_t n, const double* x) {
+  FILE* f = std::fopen(path.c_str(), "wb");
+  if (!f) return Status::CannotOpen;
+  if (ends_with(path, ".bin"))
+    std::fwrite(x, sizeof(double), (size_t)n, f);
+  else
+    for (int64_t i = 0; i < n; ++i) std::fprintf(f, "%.17g\n", x[i]);
   std::fclose(f);
   return Status::Ok;
 }

@@ -97,6 +97,16 @@ py::dict stats_to_dict(const SolveStats& st) {
   d["pivots"] = st.pivots;
   d["offdiag_pivots"] = st.offdiag_pivots;
   d["bcast_bytes"] = st.bcast_bytes;
+  if (st.profiled) {
+    py::dict ph;
+    for (int i = 0; i < kNumPhases; ++i) {
+      py::dict e;
+      e["ms"] = st.phase_ms[i];
+      e["calls"] = st.phase_calls[i];
+      ph[phase_name(i)] = e;
+    }
+    d["phases"] = ph;
+  }
   return d;
 }
 
@@ -231,10 +241,12 @@ PYBIND11_MODULE(_C, mod) {
   py::class_<PyEngine>(mod, "Engine")
       .def(py::init([](std::shared_ptr<Device> dev, std::shared_ptr<Comm> comm, int64_t n, int64_t m,
                        const std::string& dtype, int64_t chunk_cols, double eps, bool sync_debug,
-                       int depth) {
+                       int depth, bool profile, double comm_timeout_s) {
              SolveOptions o;
              o.dtype = parse_dtype(dtype);
              o.depth = depth;
+             o.profile = profile;
+             o.comm_timeout_s = comm_timeout_s;
              o.chunk_cols = chunk_cols;
              o.eps = eps;
              o.sync_debug = sync_debug;
@@ -246,7 +258,7 @@ PYBIND11_MODULE(_C, mod) {
            }),
            py::arg("device"), py::arg("comm"), py::arg("n"), py::arg("m"), py::arg("dtype") = "fp64",
            py::arg("chunk_cols") = 0, py::arg("eps") = kDefaultEps, py::arg("sync_debug") = false,
-           py::arg("depth") = 4)
+           py::arg("depth") = 4, py::arg("profile") = false, py::arg("comm_timeout_s") = 600.0)
       .def_property_readonly("layout",
                              [](PyEngine& e) {
                                const Layout& L = e.eng->layout();
@@ -339,6 +351,10 @@ PYBIND11_MODULE(_C, mod) {
     if (d.contains("eps")) c.solve.eps = d["eps"].cast<double>();
     if (d.contains("sync_debug")) c.solve.sync_debug = d["sync_debug"].cast<bool>();
     if (d.contains("depth")) c.solve.depth = d["depth"].cast<int>();
+    if (d.contains("profile")) c.solve.profile = d["profile"].cast<bool>();
+    if (d.contains("rhs")) c.rhs = d["rhs"].cast<std::string>();
+    if (d.contains("keep_solution")) c.keep_solution = d["keep_solution"].cast<bool>();
+    if (d.contains("comm_timeout_s")) c.solve.comm_timeout_s = d["comm_timeout_s"].cast<double>();
     if (d.contains("residual")) {
       const std::string r = d["residual"].cast<std::string>();
       c.residual = r == "never" ? ResidualMode::Never : r == "compat" ? ResidualMode::Compat : ResidualMode::Always;
@@ -353,6 +369,12 @@ PYBIND11_MODULE(_C, mod) {
       if (inp.ndim() != 2 || inp.shape(0) != c.n || inp.shape(1) != c.n)
         throw std::invalid_argument("input must be (n, n)");
       c.input = inp.data();
+    }
+    py::array_t<double, py::array::c_style | py::array::forcecast> rhs_in;
+    if (d.contains("rhs_input") && !d["rhs_input"].is_none()) {
+      rhs_in = d["rhs_input"].cast<py::array_t<double, py::array::c_style | py::array::forcecast>>();
+      if (rhs_in.size() != c.n) throw std::invalid_argument("rhs_input must have n entries");
+      c.rhs_input = rhs_in.data();
     }
     RunReport r;
     {
@@ -374,6 +396,12 @@ PYBIND11_MODULE(_C, mod) {
     o["device"] = r.device_desc;
     o["comm"] = r.comm_desc;
     o["gflops_nominal"] = r.gflops_nominal;
+    if (r.rhs_solved) {
+      o["axb_residual"] = r.rhs_residual;
+      o["axb_seconds"] = r.rhs_seconds;
+      o["x_head"] = r.x_head;
+      if (c.keep_solution) o["x"] = to_array(r.x, c.n, 1);
+    }
     return o;
   });
 

@@ -112,6 +112,12 @@ void HipDevice::wait(int s, int ev) {
   HIP_OK(hipStreamWaitEvent(hs(streams_[s]), static_cast<hipEvent_t>(events_[ev]), 0));
 }
 void HipDevice::sync_event(int ev) { HIP_OK(hipEventSynchronize(static_cast<hipEvent_t>(events_[ev]))); }
+bool HipDevice::query_event(int ev) {
+  const hipError_t e = hipEventQuery(static_cast<hipEvent_t>(events_[ev]));
+  if (e == hipErrorNotReady) return false;
+  HIP_OK(e);
+  return true;
+}
 void HipDevice::sync_stream(int s) { HIP_OK(hipStreamSynchronize(hs(streams_[s]))); }
 void HipDevice::sync_all() {
   for (int s = 0; s < kNumStreams; ++s) sync_stream(s);

@@ -3,6 +3,7 @@
 // Used for `gj --device cpu` (the reference's CPU-only "plumbing" configuration), for CPU tests of
 // the distributed protocol, and as an oracle.  It is never chosen implicitly for a GPU run.
 // Streams/events are no-ops: every op completes before it returns.
+#include <chrono>
 #include "gj/host_device.hpp"
 
 #include <algorithm>
@@ -129,13 +130,20 @@ void HostDevice::copy2d(void* dst, size_t dpitch, const void* src, size_t spitch
     std::memmove(static_cast<char*>(dst) + r * dpitch, static_cast<const char*>(src) + r * spitch, w);
 }
 
-int HostDevice::create_event(bool) { return nev_++; }
-void HostDevice::record(int, int) {}
+// Events carry the host time at which they were recorded (all work before them is complete).
+int HostDevice::create_event(bool) {
+  ev_time_.push_back(0.0);
+  return nev_++;
+}
+void HostDevice::record(int ev, int) {
+  ev_time_[ev] = std::chrono::duration<double, std::milli>(
+                     std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 void HostDevice::wait(int, int) {}
 void HostDevice::sync_event(int) {}
 void HostDevice::sync_stream(int) {}
 void HostDevice::sync_all() {}
-float HostDevice::event_ms(int, int) { return 0.f; }
+float HostDevice::event_ms(int a, int b) { return (float)(ev_time_[b] - ev_time_[a]); }
 
 void HostDevice::generate(DType dt, void* X, const Layout& L, GenSpec g, int) {
   parallel_for(L.rows, nthreads_, [&](int64_t r) {

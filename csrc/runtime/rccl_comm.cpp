@@ -94,6 +94,25 @@ void RcclComm::group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) {
   NCCL_OK(ncclGroupEnd());
 }
 
+void RcclComm::check_health() {
+  for (void* c : comms_) {
+    if (!c) continue;
+    ncclResult_t st = ncclSuccess;
+    NCCL_OK(ncclCommGetAsyncError(static_cast<ncclComm_t>(c), &st));
+    if (st != ncclSuccess && st != ncclInProgress)
+      throw Error(Status::CommError, std::string("RCCL asynchronous error: ") + ncclGetErrorString(st));
+  }
+}
+
+void RcclComm::abort() {
+  hipSetDevice(device_);
+  for (void*& c : comms_)
+    if (c) {
+      ncclCommAbort(static_cast<ncclComm_t>(c));
+      c = nullptr;
+    }
+}
+
 void RcclComm::barrier(Device& dev) {
   dev.sync_all();
   double v = 0.0;

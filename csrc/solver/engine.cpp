@@ -21,9 +21,12 @@
 // Nothing cancels (no I + H tricks), so the numerics match the step-by-step reference.
 #include "gj/engine.hpp"
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <thread>
 
 namespace gj {
 
@@ -143,6 +146,78 @@ void Engine::dbg_sync() {
   if (opt_.sync_debug) dev_.sync_all();
 }
 
+const char* phase_name(int ph) {
+  static const char* names[kNumPhases] = {"column",    "pivot_search", "pivot_exchange",
+                                          "owner_edits", "panel_pieces", "normalise_rows",
+                                          "row_bcast", "trailing_update", "finalize"};
+  return (ph >= 0 && ph < kNumPhases) ? names[ph] : "?";
+}
+
+// Spin on the event (the wait is on the critical path of small problems), checking the
+// communicator every 20 ms and giving up after comm_timeout_s: a dead peer turns into an error on
+// every surviving rank instead of a hang (reference: none).
+void Engine::wait_pivot(int ev, int64_t step, double& host_wait) {
+  const double w0 = now_s();
+  double next_check = w0 + 0.02;
+  int spins = 0;
+  while (!dev_.query_event(ev)) {
+    if (++spins > 2000) std::this_thread::yield();
+    const double t = now_s();
+    if (t >= next_check) {
+      comm_.check_health();
+      if (t - w0 > opt_.comm_timeout_s) {
+        comm_.abort();
+        throw Error(Status::CommError, "timed out after " + std::to_string(opt_.comm_timeout_s) +
+                                           " s waiting for the pivot of step " + std::to_string(step) +
+                                           " (peer failure or hang)");
+      }
+      next_check = t + 0.02;
+    }
+  }
+  host_wait += now_s() - w0;
+}
+
+int Engine::prof_event() {
+  if (pev_next_ == pev_pool_.size()) pev_pool_.push_back(dev_.create_event(/*timing=*/true));
+  return pev_pool_[pev_next_++];
+}
+int Engine::prof_begin(int s) {
+  if (!opt_.profile) return -1;
+  const int e = prof_event();
+  dev_.record(e, s);
+  return e;
+}
+void Engine::prof_end(int phase, int ev0, int s) {
+  if (ev0 < 0) return;
+  const int e = prof_event();
+  dev_.record(e, s);
+  pmarks_.push_back({phase, ev0, e});
+}
+void Engine::prof_collect(SolveStats& st) {
+  if (!opt_.profile) return;
+  dev_.sync_all();
+  for (const auto& mk : pmarks_) {
+    st.phase_ms[mk.phase] += dev_.event_ms(mk.ev0, mk.ev1);
+    st.phase_calls[mk.phase] += 1;
+  }
+  st.profiled = true;
+  pmarks_.clear();
+  pev_next_ = 0;
+}
+
+namespace {
+// roctx range for the host-side enqueue of a phase (visible with rocprofv3 --marker-trace)
+struct Range {
+  bool on;
+  Range(bool enabled, const char* name) : on(enabled) {
+    if (on) roctxRangePushA(name);
+  }
+  ~Range() {
+    if (on) roctxRangePop();
+  }
+};
+}  // namespace
+
 // ---------------------------------------------------------------- input
 void Engine::generate(GenSpec g) {
   dev_.generate(opt_.dtype, X_, L_, g, S_MAIN);
@@ -184,12 +259,17 @@ double Engine::norm_inf() {
 void Engine::select(int64_t t, const void* Lt) {
   const int par = (int)(t & 1);
   const double thresh = opt_.eps * norm_a_;
+  Range rg(opt_.profile, "gj:select");
+  int pe = prof_begin(S_SIDE);
   if (L_.nblk > 0)
     dev_.block_inverse(opt_.dtype, Lt, L_.rows, inv_, scores_, valid_, used_, L_, thresh, S_SIDE);
   dev_.pivot_local(scores_, valid_, used_, pos_, L_, myrec_, S_SIDE);
+  prof_end(PH_PIVOT, pe, S_SIDE);
+  pe = prof_begin(S_SIDE);
   comm_.allgather(dev_, myrec_, recs_, sizeof(PivotRec), S_SIDE);
   dev_.pivot_global(recs_, (int32_t)L_.p, (int32_t)t, pos_, phys_at_, used_, seq_, piv_dev_, S_SIDE);
   dev_.copy(&piv_host_[par], piv_dev_, sizeof(PivotResult), S_SIDE);
+  prof_end(PH_EXCHANGE, pe, S_SIDE);
   dev_.record(ev_sel_[par], S_SIDE);
   dbg_sync();
 }
@@ -219,19 +299,17 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
     } else {
       // column t after panel v-1 (look-ahead) and steps t0..t-1 of this panel
       dev_.wait(S_SIDE, ev_pp_[par][j - 1]);
+      const int pe = prof_begin(S_SIDE);
       if (rows > 0) {
         GemmExtra ex = pivot_rows_extra(par, j);
         dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, m, j * m, At_[par], rows,
                   elem(PP_[par], j * m), dm, elem(X_, t * m), npad, S_SIDE, ex);
         dev_.extract_neg_t(opt_.dtype, Lt, rows, X_, npad, rows, t * m, m, S_SIDE);
       }
+      prof_end(PH_COLUMN, pe, S_SIDE);
     }
     select(t, Lt);
-    {
-      const double w0 = now_s();
-      dev_.sync_event(ev_sel_[t & 1]);
-      host_wait += now_s() - w0;
-    }
+    wait_pivot(ev_sel_[t & 1], t, host_wait);
     const PivotResult r = piv_host_[t & 1];
     if (!r.found) {
       dev_.sync_all();
@@ -243,6 +321,7 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
     st.pivots[t] = r.phys;
     const bool owner = (r.owner == L_.k);
     const int64_t sl = r.phys / L_.p;
+    int pe = prof_begin(S_SIDE);
     if (owner) {
       st.bcast_bytes += double(m) * npad * es;
       if (j > 0)  // multipliers of row s_t for steps t0..t-1 (K-major j*m x m)
@@ -252,11 +331,13 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
       dev_.memset2d(elem(At_[par], sl * m), rows * es, m * es, (j + 1) * m, S_SIDE);
       dev_.add_diag(opt_.dtype, elem(At_[par], j * m * rows + sl * m), rows, m, 1.0, S_SIDE);
     }
+    prof_end(PH_EDITS, pe, S_SIDE);
     dev_.record(ev_edit_[par], S_SIDE);
     dbg_sync();
 
     // panel piece PP_t (m x q*m, ld dm) on COMM
     dev_.wait(S_COMM, ev_edit_[par]);
+    pe = prof_begin(S_COMM);
     void* pp = elem(PP_[par], j * m * dm);
     if (owner) {
       for (int64_t jc = 0; jc < q; ++jc) {
@@ -279,6 +360,7 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
       dev_.h_block(opt_.dtype, elem(pp, j * m), dm, Ht_[par][j], m, S_COMM);
     }
     comm_.bcast(dev_, pp, (size_t)m * dm * es, r.owner, S_COMM);
+    prof_end(PH_PIECES, pe, S_COMM);
     dev_.record(ev_pp_[par][j], S_COMM);
     dbg_sync();
   }
@@ -315,6 +397,7 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
     for (int64_t j = 0; j < q; ++j) {
       const PivotResult& r = piv_[par][j];
       char* seg = chunk + j * m * W * (int64_t)es;
+      int pe = prof_begin(S_COMM);
       if (r.owner == L_.k) {
         const int64_t sl = r.phys / L_.p;
         for (int64_t z = 0; z < nr; ++z) {
@@ -338,7 +421,10 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
             dev_.memset2d(dst + (j + 1) * m * (int64_t)es, W * es, (q - j - 1) * m * es, m, S_COMM);
         }
       }
+      prof_end(PH_NORMALISE, pe, S_COMM);
+      pe = prof_begin(S_COMM);
       comm_.bcast(dev_, seg, (size_t)m * W * es, r.owner, S_COMM);
+      prof_end(PH_BCAST, pe, S_COMM);
     }
     dev_.record(ev_b_[par][c], S_COMM);
   }
@@ -361,12 +447,14 @@ void Engine::big_update(int64_t u) {
     x0 = tn * m;
     x1 = (tn + qn) * m;
     dev_.wait(S_MAIN, ev_b_[par][cn]);
+    const int pe = prof_begin(S_MAIN);
     if (rows > 0) {
       dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, x1 - x0, K, At_[par], rows,
                 rb_chunk(par, cn) + (x0 - cb0_[cn] * m) * (int64_t)esz(), chunk_w(cn), elem(X_, x0),
                 npad, S_MAIN, prows);
       dev_.extract_neg_t(opt_.dtype, At_[npar], rows, X_, npad, rows, x0, m, S_MAIN);
     }
+    prof_end(PH_UPDATE, pe, S_MAIN);
     dev_.record(ev_L_, S_MAIN);
     dbg_sync();
   }
@@ -376,6 +464,7 @@ void Engine::big_update(int64_t u) {
     const int64_t c = (start + i) % C;
     const int64_t c0 = cb0_[c] * m, c1 = cb1_[c] * m, W = c1 - c0;
     dev_.wait(S_MAIN, ev_b_[par][c]);
+    const int pe = prof_begin(S_MAIN);
     int64_t ra[2], rb[2], nr = 0;
     if (has_next && x0 >= c0 && x0 < c1) {
       if (x0 > c0) { ra[nr] = c0; rb[nr] = x0; ++nr; }
@@ -392,6 +481,7 @@ void Engine::big_update(int64_t u) {
                   rb_chunk(par, c) + (ra[z] - c0) * (int64_t)esz(), W, elem(X_, ra[z]), npad, S_MAIN,
                   ex);
       }
+    prof_end(PH_UPDATE, pe, S_MAIN);
     dev_.record(ev_c_[c], S_MAIN);
   }
   dbg_sync();
@@ -402,6 +492,8 @@ SolveStats Engine::solve() {
   GJ_REQUIRE(!solved_, "solve(): input panel already consumed; load the matrix again");
   SolveStats st;
   const int64_t m = L_.m, Nr = L_.Nr, rows = L_.rows, npad = L_.npad;
+  pmarks_.clear();
+  pev_next_ = 0;
 
   comm_.barrier(dev_);
   const double t_begin = now_s();
@@ -444,13 +536,18 @@ SolveStats Engine::solve() {
     return st;
   }
 
-  finalize(st.pivots);
+  {
+    const int pe = prof_begin(S_COMM);
+    finalize(st.pivots);
+    prof_end(PH_FINALIZE, pe, S_COMM);
+  }
   dev_.sync_all();
   const double t_end = now_s();
   for (int64_t t = 0; t < Nr; ++t)
     if (st.pivots[t] != t) st.offdiag_pivots++;
   st.host_wait_ms = host_wait * 1e3;
   st.seconds = t_end - t_begin;
+  prof_collect(st);
   solved_ = true;
   return st;
 }
@@ -605,6 +702,69 @@ double Engine::residual_rows(const double* host, int64_t ld) {
   upload_local_rows(host, ld);
   solved_ = true;
   return residual_common();
+}
+
+// ---------------------------------------------------------------- A x = b
+namespace {
+// full n-vector (double, host) -> padded device vector of the engine dtype
+void* upload_vector(Device& dev, DType dt, const double* v, int64_t n, int64_t npad) {
+  double* st = static_cast<double*>(dev.alloc(sizeof(double) * npad));
+  dev.memset0(st, sizeof(double) * npad, S_MAIN);
+  dev.copy(st, v, sizeof(double) * n, S_MAIN);
+  void* d = dev.alloc(dtype_size(dt) * npad);
+  dev.upload_convert(dt, d, 1, st, 1, npad, 1, S_MAIN);
+  dev.sync_stream(S_MAIN);
+  dev.release(st);
+  return d;
+}
+}  // namespace
+
+// local product y = P * v  (P: this rank's rows of a panel, v: full padded vector) -> host doubles
+static std::vector<double> local_matvec(Device& dev, DType dt, const void* P, const Layout& L,
+                                        const void* vd) {
+  const size_t es = dtype_size(dt);
+  std::vector<double> y((size_t)L.rows, 0.0);
+  if (L.rows == 0) return y;
+  void* yd = dev.alloc(es * L.rows);
+  dev.gemm(dt, GemmOp::Store, ALayout::RowMajor, L.rows, 1, L.npad, P, L.npad, vd, 1, yd, 1, S_MAIN);
+  std::vector<char> h(es * L.rows);
+  dev.copy(h.data(), yd, es * L.rows, S_MAIN);
+  dev.sync_stream(S_MAIN);
+  dev.release(yd);
+  for (int64_t i = 0; i < L.rows; ++i)
+    y[i] = dt == DType::F64 ? reinterpret_cast<double*>(h.data())[i] : (double)reinterpret_cast<float*>(h.data())[i];
+  return y;
+}
+
+void Engine::apply_inverse(const double* b, double* x) {
+  GJ_REQUIRE(solved_, "apply_inverse: solve() first");
+  const int64_t m = L_.m, n = L_.n, p = L_.p;
+  void* bd = upload_vector(dev_, opt_.dtype, b, n, L_.npad);
+  std::vector<double> mine = local_matvec(dev_, opt_.dtype, out_, L_, bd);
+  dev_.release(bd);
+  const int64_t per = L_.max_nblk * m;
+  mine.resize((size_t)per, 0.0);
+  std::vector<double> all((size_t)per * p);
+  comm_.host_allgather(dev_, mine.data(), all.data(), sizeof(double) * per);
+  for (int64_t q = 0; q < p; ++q)
+    for (int64_t j = 0; j < rows_owned(L_.Nr, p, q); ++j)
+      for (int64_t r = 0; r < m; ++r) {
+        const int64_t gi = (j * p + q) * m + r;
+        if (gi < n) x[gi] = all[(size_t)q * per + j * m + r];
+      }
+}
+
+double Engine::axb_residual(const double* x, const double* b) {
+  const int64_t m = L_.m, n = L_.n;
+  void* xd = upload_vector(dev_, opt_.dtype, x, n, L_.npad);
+  std::vector<double> y = local_matvec(dev_, opt_.dtype, X_, L_, xd);
+  dev_.release(xd);
+  double local = 0.0;
+  for (int64_t i = 0; i < L_.rows; ++i) {
+    const int64_t gi = L_.global_block(i / m) * m + i % m;
+    if (gi < n) local = std::max(local, std::fabs(y[i] - b[gi]));
+  }
+  return comm_.host_max(dev_, local);
 }
 
 void SelfComm::host_allgather(Device&, const void* send, void* recv, size_t bytes) {

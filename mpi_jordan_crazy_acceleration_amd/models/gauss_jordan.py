@@ -60,13 +60,21 @@ class GaussJordan:
         return cfg
 
     def run(self, n: int, gen: str = "absdiff", seed: int = 0, file: Optional[str] = None,
-            input: Optional[np.ndarray] = None, keep_inverse: bool = False, repeats: int = 1) -> dict:
+            input: Optional[np.ndarray] = None, keep_inverse: bool = False, repeats: int = 1,
+            rhs=None, keep_solution: bool = False, profile: bool = False) -> dict:
+        """One CLI-equivalent run.  ``rhs``: None, "ones", "random", a file path, or an n-vector —
+        then x = inv(A) b is computed on the devices and ``axb_residual`` = ||A x - b||_inf reported."""
         cfg = self._cfg(n)
-        cfg.update(gen=gen, seed=int(seed), keep_inverse=keep_inverse, repeats=int(repeats))
+        cfg.update(gen=gen, seed=int(seed), keep_inverse=keep_inverse, repeats=int(repeats),
+                   keep_solution=bool(keep_solution), profile=bool(profile))
         if file is not None:
             cfg["file"] = str(file)
         if input is not None:
             cfg["input"] = np.ascontiguousarray(input, dtype=np.float64)
+        if isinstance(rhs, str):
+            cfg["rhs"] = rhs
+        elif rhs is not None:
+            cfg["rhs_input"] = np.ascontiguousarray(np.asarray(rhs, dtype=np.float64).reshape(-1))
         rep = load_native().run_local(cfg)
         rep["status_name"] = STATUS.get(rep["status"], "error")
         return rep
@@ -93,7 +101,22 @@ def inverse(A, block_size: int = 128, **kw):
 
 
 def solve(A, b, block_size: int = 128, **kw):
-    """Solve ``A x = b`` (b: vector or matrix of right-hand sides) via the block Gauss-Jordan inverse."""
+    """Solve ``A x = b`` via the block Gauss-Jordan inverse.
+
+    A single right-hand side runs the native path (x = inv(A) b on the devices, the GEMV next to
+    the inverse's rows); a matrix of right-hand sides multiplies by the returned inverse."""
+    is_torch = isinstance(A, torch.Tensor)
+    bn = b.detach().cpu().numpy() if isinstance(b, torch.Tensor) else np.asarray(b, dtype=np.float64)
+    if bn.ndim == 1:
+        a = A.detach().to("cpu", torch.float64).numpy() if is_torch else np.asarray(A, dtype=np.float64)
+        gj = GaussJordan(block_size=block_size, residual="never", **kw)
+        rep = gj.run(a.shape[0], input=a, rhs=bn, keep_solution=True)
+        if rep["status"] == 1:
+            raise SingularMatrixError("singular matrix")
+        if rep["status"] != 0:
+            raise RuntimeError(rep["message"] or rep["status_name"])
+        x = rep["x"].reshape(-1)
+        return torch.from_numpy(x).to(device=A.device, dtype=A.dtype) if is_torch else x
     inv = inverse(A, block_size=block_size, **kw)
     if isinstance(inv, torch.Tensor):
         return inv @ (b if isinstance(b, torch.Tensor) else torch.as_tensor(b, dtype=inv.dtype))

@@ -104,3 +104,43 @@ def test_binary_input(gj_bin, tmp_path):
     assert rc == 0
     inv = np.fromfile(out_f, dtype="<f8").reshape(n, n)
     assert np.abs(inv - np.linalg.inv(A)).max() < 1e-10
+
+
+def test_axb_plumbing_512(gj_bin, tmp_path):
+    """BASELINE config 1: 512x512 random dense A x = b, one rank, CPU."""
+    xf = tmp_path / "x.txt"
+    rc, out, err = run(gj_bin, "--gen", "random", "--seed", 5, "--rhs", "random", "--out-x", xf, "--json", 512, 64)
+    assert rc == 0, err
+    assert "Ax-b residual:" in out
+    res = float(out.strip().split("\n")[-1].split()[-1])
+    assert res < 1e-10
+    x = np.loadtxt(xf)
+    A = generate_matrix(512, "random", 5)
+    assert np.abs(A @ x).max() > 0
+    assert '"axb_residual"' in err
+
+
+def test_axb_rhs_file(gj_bin, tmp_path):
+    n = 40
+    A = generate_matrix(n, "random", 3)
+    b = np.arange(n, dtype=float) - 7.5
+    af, bf, xf = tmp_path / "a.txt", tmp_path / "b.txt", tmp_path / "x.bin"
+    np.savetxt(af, A, fmt="%.17g")
+    np.savetxt(bf, b, fmt="%.17g")
+    rc, out, _ = run(gj_bin, "-p", 3, "--rhs", bf, "--out-x", xf, n, 6, af)
+    assert rc == 0
+    x = np.fromfile(xf, dtype="<f8")
+    assert np.allclose(x, np.linalg.solve(A, b), rtol=1e-9, atol=1e-11)
+    rc, out, _ = run(gj_bin, "--rhs", tmp_path / "missing.txt", n, 6, af)
+    assert rc == 2 and out == f"cannot open {tmp_path / 'missing.txt'}\n"
+
+
+def test_profile_json_phases(gj_bin):
+    rc, out, err = run(gj_bin, "-p", 2, "--profile", "--json", 200, 16)
+    assert rc == 0
+    import json
+    rep = json.loads(err.strip().split("\n")[-1])
+    ph = rep["phases_ms"]
+    assert set(ph) == {"column", "pivot_search", "pivot_exchange", "owner_edits", "panel_pieces",
+                       "normalise_rows", "row_bcast", "trailing_update", "finalize"}
+    assert ph["trailing_update"] > 0

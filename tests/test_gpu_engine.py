@@ -10,7 +10,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("n,m", [(1000, 128), (517, 60), (64, 64), (300, 256), (10, 12), (40, 1)])
 @pytest.mark.parametrize("gen", ["random", "absdiff"])
-@pytest.mark.parametrize("depth", [1, 2, 3])
+@pytest.mark.parametrize("depth", [1, 2, 3, 4])
 def test_engine_single_gpu_vs_numpy(native, n, m, gen, depth):
     eng = native.Engine(native.hip_device(0), native.self_comm(), n, m, "fp64", 0, 1e-15, False, depth)
     eng.generate(gen, 5)
@@ -79,3 +79,34 @@ def test_sync_debug_equals_async(native):
         assert eng.solve()["status"] == 0
         outs.append(eng.download_local_rows())
     assert np.array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("ranks", [1, 2])
+def test_axb_and_profile_on_gpu(native, ranks):
+    n, m = 777, 64
+    A = generate_matrix(n, "random", 13)
+    b = np.linspace(-1, 1, n)
+    rep = gj.GaussJordan(block_size=m, ranks=ranks, device="gpu", comm="auto" if ranks == 1 else "loopback").run(
+        n, input=A, rhs=b, keep_solution=True, profile=True)
+    assert rep["status"] == 0
+    x = rep["x"].reshape(-1)
+    assert np.allclose(x, np.linalg.solve(A, b), rtol=1e-8, atol=1e-10)
+    assert rep["axb_residual"] < 1e-9
+    ph = rep["stats"]["phases"]
+    assert ph["trailing_update"]["ms"] > 0 and ph["pivot_search"]["calls"] == (n + m - 1) // m
+
+
+@pytest.mark.parametrize("variant", ["panel", "sweep"])
+def test_block_inverse_variants_in_engine(native, variant):
+    n, m = 640, 128
+    A = generate_matrix(n, "random", 21)[::-1].copy()  # forces off-diagonal pivots
+    native.set_block_inverse_variant(variant)
+    try:
+        eng = native.Engine(native.hip_device(0), native.self_comm(), n, m, "fp64")
+        eng.upload_local_rows(A)
+        st = eng.solve()
+    finally:
+        native.set_block_inverse_variant("panel")
+    inv_ref, _ = gauss_jordan_reference(A, m, 1)
+    assert st["offdiag_pivots"] > 0
+    assert np.abs(eng.download_local_rows() - inv_ref).max() / np.abs(inv_ref).max() < 1e-9

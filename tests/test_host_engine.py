@@ -152,3 +152,22 @@ def test_host_gemm_extras_match_torch():
     ref = Cin + A @ B
     ops.gemm(A.t().contiguous(), B, C, op="acc", a_kmajor=True, zero_cols=(5, 25), zero_rows=[30], zero_row_height=10)
     assert (C - ref).abs().max().item() < 1e-12
+
+
+def test_python_solve_vector_native_path(native):
+    import mpi_jordan_crazy_acceleration_amd as gj
+    rng = np.random.default_rng(11)
+    A = rng.standard_normal((70, 70))
+    b = rng.standard_normal(70)
+    x = gj.solve(A, b, block_size=16, device="cpu", ranks=3)
+    assert np.abs(A @ x - b).max() < 1e-10
+    X = gj.solve(A, np.stack([b, 2 * b], 1), block_size=16, device="cpu")
+    assert np.allclose(X[:, 1], 2 * x, atol=1e-9)
+
+
+def test_engine_profile_phases(native):
+    rep = native.run_local(dict(n=150, m=16, ranks=2, device="cpu", gen="random", profile=True,
+                                rhs="ones"))
+    ph = rep["stats"]["phases"]
+    assert ph["trailing_update"]["calls"] > 0 and ph["pivot_search"]["calls"] == 10
+    assert rep["axb_residual"] < 1e-10
