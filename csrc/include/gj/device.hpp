@@ -40,6 +40,9 @@ struct GemmExtra {
   int nzr = 0;
   int64_t zr[kMaxZeroRows] = {0, 0, 0, 0};
   int64_t zh = 0;
+  // Few-tile GEMM on the panel-factorisation critical path: prefer small tiles (more workgroups,
+  // shorter K loop per workgroup) over the throughput tiles of the trailing update.
+  bool latency = false;
 };
 
 class Device {

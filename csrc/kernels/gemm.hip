@@ -54,6 +54,7 @@ struct Cfg {
 using CfgBig = Cfg<128, 128, 16, 2, 4, 2>;   // 512 threads, 2 WG/CU (73.7 KiB LDS each)
 using CfgNarrow = Cfg<128, 64, 8, 2, 2, 4>;  // 256 threads, 4 WG/CU (28.7 KiB LDS each)
 using CfgTall = Cfg<64, 128, 8, 1, 4, 4>;    // 256 threads, 4 WG/CU
+using CfgSmall = Cfg<64, 32, 16, 2, 1, 8>;   // 128 threads: latency-bound panel GEMMs (few tiles)
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
@@ -122,6 +123,7 @@ struct GemmArgs {
   int64_t n_real, blk_m, p, k;
   double* partial;  // [M][nparts]
   int nparts;
+  bool latency;     // GemmExtra::latency -> CfgSmall for few-tile launches
 };
 
 // XCD-aware bijective remap: blocks b and b+8 share an XCD (MI355X_MICROARCH.md §Workgroup
@@ -330,9 +332,16 @@ int gemm_variant_id(const char* name) {
 }
 void set_gemm_variant(int v) { g_variant = v; }
 
+// Below this many narrow tiles the GEMM cannot fill the 256 CUs: use 8x smaller tiles instead
+// (the panel-factorisation GEMMs: m x m .. m x d*m outputs, or rows x m column updates).
+constexpr int64_t kSmallGridTiles = 512;
+
 template <typename T, int AL, int MODE>
 static void launch(const GemmArgs& a, hipStream_t s) {
   if (MODE == MODE_RESID) return launch_cfg<T, AL, MODE, CfgBig>(a, s);
+  const int64_t narrow_tiles = ((a.M + CfgNarrow::BM - 1) / CfgNarrow::BM) * ((a.N + CfgNarrow::BN - 1) / CfgNarrow::BN);
+  if (a.latency && narrow_tiles < kSmallGridTiles && gemm_variant() != 0)
+    return launch_cfg<T, AL, MODE, CfgSmall>(a, s);
   switch (gemm_variant()) {
     case 1: return launch_cfg<T, AL, MODE, CfgNarrow>(a, s);
     case 2: return launch_cfg<T, AL, MODE, CfgTall>(a, s);
@@ -347,6 +356,7 @@ static void fill_extra(GemmArgs& a, const GemmExtra* ex) {
   a.zc1 = ex ? ex->zc1 : 0;
   a.zh = ex ? ex->zh : 0;
   for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) a.zr[z] = (ex && z < ex->nzr) ? ex->zr[z] : kNone;
+  a.latency = ex ? ex->latency : false;
 }
 
 void gemm(DType dt, int op, int a_kmajor, int64_t M, int64_t N, int64_t K, const void* A,

@@ -46,7 +46,7 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
 
   // Column chunk plan: fixed partition of the Nr block columns into runs of a multiple of d blocks.
   int64_t target_cols = opt_.chunk_cols;
-  if (target_cols <= 0) target_cols = std::max<int64_t>(2048, (L_.npad + 7) / 8);
+  if (target_cols <= 0) target_cols = std::max<int64_t>(4096, (L_.npad + 7) / 8);
   int64_t cw = std::max<int64_t>(1, target_cols / m);
   cw = ((cw + d_ - 1) / d_) * d_;
   for (int64_t b = 0; b < L_.Nr; b += cw) {
@@ -302,6 +302,7 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
       const int pe = prof_begin(S_SIDE);
       if (rows > 0) {
         GemmExtra ex = pivot_rows_extra(par, j);
+        ex.latency = true;
         dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, m, j * m, At_[par], rows,
                   elem(PP_[par], j * m), dm, elem(X_, t * m), npad, S_SIDE, ex);
         dev_.extract_neg_t(opt_.dtype, Lt, rows, X_, npad, rows, t * m, m, S_SIDE);
@@ -339,6 +340,8 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
     dev_.wait(S_COMM, ev_edit_[par]);
     pe = prof_begin(S_COMM);
     void* pp = elem(PP_[par], j * m * dm);
+    GemmExtra lat;
+    lat.latency = true;
     if (owner) {
       for (int64_t jc = 0; jc < q; ++jc) {
         if (jc == j) continue;
@@ -346,17 +349,17 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
         if (jc < j) {  // earlier pivot column: sum over steps jc..j-1 only, no input
           dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, m, (j - jc) * m,
                     elem(Lrow_[par][j], jc * m * m), m, elem(PP_[par], jc * m * dm + jc * m), dm, rp,
-                    dm, S_COMM);
+                    dm, S_COMM, lat);
         } else {  // later panel column: look-ahead value + all earlier steps
           dev_.copy2d(rp, dm * es, elem(X_, sl * m * npad + (t0 + jc) * m), npad * es, m * es, m,
                       S_COMM);
           if (j > 0)
             dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, m, m, j * m, Lrow_[par][j], m,
-                      elem(PP_[par], jc * m), dm, rp, dm, S_COMM);
+                      elem(PP_[par], jc * m), dm, rp, dm, S_COMM, lat);
         }
       }
       dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, q * m, m, Ht_[par][j], m, RP_, dm, pp,
-                dm, S_COMM);
+                dm, S_COMM, lat);
       dev_.h_block(opt_.dtype, elem(pp, j * m), dm, Ht_[par][j], m, S_COMM);
     }
     comm_.bcast(dev_, pp, (size_t)m * dm * es, r.owner, S_COMM);

@@ -16,7 +16,7 @@ def _rand(shape, dtype, seed):
 
 
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
-@pytest.mark.parametrize("M,N,K", [(128, 128, 128), (256, 384, 128), (300, 200, 60), (37, 515, 17), (1000, 130, 256)])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 128), (256, 384, 128), (300, 200, 60), (37, 515, 17), (1000, 130, 256), (2100, 1600, 136)])
 @pytest.mark.parametrize("kmajor", [True, False])
 def test_gemm_acc_matches_torch(dtype, M, N, K, kmajor):
     A = _rand((M, K), dtype, 1)
@@ -125,7 +125,7 @@ def test_row_abs_max_and_residual():
 
 
 @pytest.mark.parametrize("variant", ["big", "narrow", "tall", "valu"])
-@pytest.mark.parametrize("M,N,K", [(256, 384, 128), (300, 200, 60), (1000, 130, 256)])
+@pytest.mark.parametrize("M,N,K", [(256, 384, 128), (300, 200, 60), (1000, 130, 256), (2100, 1600, 136)])
 def test_gemm_variants_elimination_extras(native, variant, M, N, K):
     """All kernel variants: C += A B where C enters as 0 in a column range and in two row blocks."""
     native.set_gemm_variant(variant)
