@@ -58,6 +58,7 @@ class LoopbackHub {
   std::vector<const void*> ptr;
   std::vector<double> val;
   std::vector<std::vector<P2POp>> p2p;  // per source rank
+  std::vector<std::string> sig;          // per rank: signature of the collective being entered
 
  private:
   int p_;
@@ -83,6 +84,10 @@ class LoopbackComm : public Comm {
   void host_allgather(Device& dev, const void* send, void* recv, size_t bytes) override;
 
  private:
+  // SPMD consistency check: every rank must enter the same collective (kind,
+  // size, root, stream role) at the same point of its program, as RCCL requires; a divergence
+  // throws on every rank instead of silently exchanging the wrong buffers.
+  void enter(const std::string& signature);
   std::shared_ptr<LoopbackHub> hub_;
   int r_;
 };

@@ -74,6 +74,10 @@ class Device {
   virtual void sync_all() = 0;
   virtual float event_ms(int ev_start, int ev_end) = 0;
   virtual void* native_stream(int s) = 0;  // hipStream_t (nullptr on host)
+  // Keep the MAIN (trailing-update) stream off `n` CUs so the latency-critical SIDE/COMM kernels
+  // always find idle CUs (mode 0: CUs 0..n-1 of the mask, mode 1: spread over the mask).
+  // Returns the number of CUs actually reserved.  Call while the device is idle.
+  virtual int reserve_cus(int n, int mode) { (void)n; (void)mode; return 0; }
 
   // ---- kernels ----
   // X (layout.rows x npad, ld npad) := A' restricted to this rank's block rows.

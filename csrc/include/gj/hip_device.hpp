@@ -31,6 +31,11 @@ class HipDevice : public Device {
   void wait(int s, int ev) override;
   void sync_event(int ev) override;
   bool query_event(int ev) override;
+ private:
+  int reserved_ = 0, reserve_mode_ = 0;
+
+ public:
+  int reserve_cus(int n, int mode) override;
   void sync_stream(int s) override;
   void sync_all() override;
   float event_ms(int ev_start, int ev_end) override;

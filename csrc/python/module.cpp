@@ -3,6 +3,8 @@
 // shares the HIP runtime / RCCL already loaded by torch (the package imports torch first).
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
+
+#include <thread>
 #include <pybind11/stl.h>
 
 #include <hip/hip_runtime.h>
@@ -227,6 +229,26 @@ PYBIND11_MODULE(_C, mod) {
     auto* sc = dynamic_cast<ShadowComm*>(c.get());
     GJ_REQUIRE(sc != nullptr, "shadow_reset: not a shadow communicator");
     sc->reset();
+  });
+  // Two virtual ranks on the host enter collectives with different roots (rank 1 passes root_b):
+  // returns the error message the loopback consistency check raised on each rank ("" = none).
+  mod.def("loopback_mismatch_probe", [](int root_b) {
+    auto hub = std::make_shared<LoopbackHub>(2);
+    std::vector<std::string> msg(2);
+    std::vector<std::thread> th;
+    for (int r = 0; r < 2; ++r)
+      th.emplace_back([&, r] {
+        HostDevice dev(1);
+        LoopbackComm c(hub, r);
+        double buf[4] = {double(r), 0, 0, 0};
+        try {
+          c.bcast(dev, buf, sizeof(buf), r == 1 ? root_b : 0, S_COMM);
+        } catch (const std::exception& e) {
+          msg[r] = e.what();
+        }
+      });
+    for (auto& t : th) t.join();
+    return msg;
   });
   mod.def("py_comm", [](py::object impl, int rank, int size) {
     return std::shared_ptr<Comm>(new PyComm(std::move(impl), rank, size));

@@ -53,6 +53,36 @@ HipDevice::~HipDevice() {
 
 void HipDevice::activate() const { hipSetDevice(dev_); }
 
+int HipDevice::reserve_cus(int n, int mode) {
+  if (n == reserved_ && mode == reserve_mode_) return reserved_;
+  activate();
+  hipDeviceProp_t prop;
+  HIP_OK(hipGetDeviceProperties(&prop, dev_));
+  const int ncu = prop.multiProcessorCount;
+  n = std::max(0, std::min(n, ncu / 2));
+  HIP_OK(hipStreamSynchronize(hs(streams_[S_MAIN])));
+  HIP_OK(hipStreamDestroy(hs(streams_[S_MAIN])));
+  hipStream_t st;
+  if (n == 0) {
+    int lo = 0, hi = 0;
+    HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIP_OK(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, lo));
+  } else {
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    for (int c = 0; c < ncu; ++c) mask[c / 32] |= 1u << (c % 32);
+    const int stride = std::max(1, ncu / n);
+    for (int i = 0; i < n; ++i) {
+      const int c = (mode == 0) ? i : i * stride;
+      mask[c / 32] &= ~(1u << (c % 32));
+    }
+    HIP_OK(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+  }
+  streams_[S_MAIN] = st;
+  reserved_ = n;
+  reserve_mode_ = mode;
+  return n;
+}
+
 std::string HipDevice::describe() const {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, dev_) != hipSuccess) return "hip:" + std::to_string(dev_);

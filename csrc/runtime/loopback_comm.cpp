@@ -8,7 +8,7 @@
 
 namespace gj {
 
-LoopbackHub::LoopbackHub(int p) : ptr(p, nullptr), val(p, 0.0), p2p(p), p_(p) {}
+LoopbackHub::LoopbackHub(int p) : ptr(p, nullptr), val(p, 0.0), p2p(p), sig(p), p_(p) {}
 
 void LoopbackHub::arrive_and_wait() {
   std::unique_lock<std::mutex> lk(mu_);
@@ -22,8 +22,23 @@ void LoopbackHub::arrive_and_wait() {
   }
 }
 
+void LoopbackComm::enter(const std::string& signature) {
+  hub_->sig[r_] = signature;
+  hub_->arrive_and_wait();
+  for (int q = 0; q < size(); ++q)
+    if (hub_->sig[q] != hub_->sig[0])
+      throw Error(Status::CommError, "collective mismatch: rank " + std::to_string(q) + " entered " +
+                                         hub_->sig[q] + " while rank 0 entered " + hub_->sig[0]);
+}
+
+static std::string sig(const char* kind, size_t bytes, int root, int s) {
+  return std::string(kind) + "(" + std::to_string(bytes) + " B, root " + std::to_string(root) +
+         ", stream " + std::to_string(s) + ")";
+}
+
 void LoopbackComm::allgather(Device& dev, const void* send, void* recv, size_t bytes, int s) {
   dev.sync_stream(s);
+  enter(sig("allgather", bytes, -1, s));
   hub_->ptr[r_] = send;
   hub_->arrive_and_wait();
   for (int q = 0; q < size(); ++q)
@@ -34,6 +49,7 @@ void LoopbackComm::allgather(Device& dev, const void* send, void* recv, size_t b
 
 void LoopbackComm::bcast(Device& dev, void* buf, size_t bytes, int root, int s) {
   dev.sync_stream(s);
+  enter(sig("bcast", bytes, root, s));
   hub_->ptr[r_] = buf;
   hub_->arrive_and_wait();
   if (r_ != root) dev.copy(buf, hub_->ptr[root], bytes, s);
@@ -43,6 +59,7 @@ void LoopbackComm::bcast(Device& dev, void* buf, size_t bytes, int root, int s) 
 
 void LoopbackComm::allreduce_max(Device& dev, double* buf, size_t count, int s) {
   dev.sync_stream(s);
+  enter(sig("allreduce_max", count * sizeof(double), -1, s));
   std::vector<double> mine(count), tmp(count);
   dev.copy(mine.data(), buf, count * sizeof(double), s);
   dev.sync_stream(s);
@@ -59,6 +76,7 @@ void LoopbackComm::allreduce_max(Device& dev, double* buf, size_t count, int s) 
 
 void LoopbackComm::group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) {
   dev.sync_stream(s);
+  enter(sig("group_p2p", 0, -1, s));
   auto& mine = hub_->p2p[r_];
   mine.clear();
   for (const auto& op : ops)
@@ -86,6 +104,7 @@ void LoopbackComm::barrier(Device& dev) {
 }
 
 double LoopbackComm::host_max(Device&, double v) {
+  enter("host_max");
   hub_->val[r_] = v;
   hub_->arrive_and_wait();
   double m = hub_->val[0];
@@ -95,6 +114,7 @@ double LoopbackComm::host_max(Device&, double v) {
 }
 
 void LoopbackComm::host_allgather(Device&, const void* send, void* recv, size_t bytes) {
+  enter(sig("host_allgather", bytes, -1, -1));
   hub_->ptr[r_] = send;
   hub_->arrive_and_wait();
   for (int q = 0; q < size(); ++q)

@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -58,6 +59,13 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
     for (int64_t b = cb0_[c]; b < cb1_[c]; ++b) chunk_of_[b] = (int64_t)c;
 
   alloc_buffers();
+
+  // CU reservation for the latency-bound panel factorisation (GJ_RESERVE_CUS overrides).
+  int rc = opt_.reserve_cus;
+  if (const char* e = std::getenv("GJ_RESERVE_CUS")) rc = std::atoi(e);
+  if (const char* e = std::getenv("GJ_RESERVE_MODE")) opt_.reserve_mode = std::atoi(e);
+  if (rc < 0) rc = 0;  // auto: off until measured otherwise
+  dev_.reserve_cus(rc, opt_.reserve_mode);
 }
 
 Engine::~Engine() { free_buffers(); }

@@ -171,3 +171,10 @@ def test_engine_profile_phases(native):
     ph = rep["stats"]["phases"]
     assert ph["trailing_update"]["calls"] > 0 and ph["pivot_search"]["calls"] == 10
     assert rep["axb_residual"] < 1e-10
+
+
+def test_loopback_detects_collective_mismatch(native):
+    ok = native.loopback_mismatch_probe(0)
+    assert ok == ["", ""]
+    bad = native.loopback_mismatch_probe(1)
+    assert all("collective mismatch" in m for m in bad), bad
