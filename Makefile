@@ -33,7 +33,12 @@ PYMOD     := $(PKG)/_C$(PYEXT)
 
 HEADERS   := $(wildcard csrc/include/gj/*.hpp) csrc/kernels/kernels.hpp
 
-.PHONY: all cli py clean
+# Host-code sanitizer build: the host runtime, engine, communicators and I/O
+# under ASan + UBSan; device code is not instrumented (GPU sanitizers are not available here).
+SANFLAGS  := -fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-frame-pointer -fno-gpu-sanitize
+ASANOBJ   := $(patsubst %,$(BUILD)/asan/%.o,$(HOST_SRC) cli/main)
+
+.PHONY: all cli py clean asan
 all: cli py
 cli: $(BUILD)/gj
 py: $(PYMOD)
@@ -59,6 +64,13 @@ $(BUILD)/gj: $(CORE) $(BUILD)/cli/main.o
 
 $(PYMOD): $(CORE) $(BUILD)/python/module.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ $(LDLIBS)
+
+asan: $(BUILD)/gj_asan
+$(BUILD)/asan/%.o: csrc/%.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HOSTFLAGS) -O1 $(SANFLAGS) -c $< -o $@
+$(BUILD)/gj_asan: $(KOBJ) $(ASANOBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -fsanitize=address,undefined -fno-gpu-sanitize -o $@ $^ $(LDLIBS) -Wl,-rpath,$(ROCM)/lib
 
 clean:
 	rm -rf $(BUILD) $(PKG)/_C*.so

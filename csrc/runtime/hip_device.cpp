@@ -43,15 +43,15 @@ HipDevice::HipDevice(int device_index) : dev_(device_index) {
 
 HipDevice::~HipDevice() {
   activate();
-  hipDeviceSynchronize();
-  for (void* e : events_) hipEventDestroy(static_cast<hipEvent_t>(e));
+  (void)hipDeviceSynchronize();
+  for (void* e : events_) (void)hipEventDestroy(static_cast<hipEvent_t>(e));
   for (void* s : streams_)
-    if (s) hipStreamDestroy(hs(s));
+    if (s) (void)hipStreamDestroy(hs(s));
   for (void* p : scratch_)
-    if (p) hipFree(p);
+    if (p) (void)hipFree(p);
 }
 
-void HipDevice::activate() const { hipSetDevice(dev_); }
+void HipDevice::activate() const { (void)hipSetDevice(dev_); }
 
 int HipDevice::reserve_cus(int n, int mode) {
   if (n == reserved_ && mode == reserve_mode_) return reserved_;
@@ -99,14 +99,14 @@ void* HipDevice::alloc(size_t bytes) {
 }
 void HipDevice::release(void* p) {
   activate();
-  hipFree(p);
+  (void)hipFree(p);
 }
 void* HipDevice::alloc_pinned(size_t bytes) {
   void* p = nullptr;
   HIP_OK(hipHostMalloc(&p, bytes ? bytes : 64, hipHostMallocDefault));
   return p;
 }
-void HipDevice::release_pinned(void* p) { hipHostFree(p); }
+void HipDevice::release_pinned(void* p) { (void)hipHostFree(p); }
 size_t HipDevice::free_memory() const {
   activate();
   size_t fr = 0, tot = 0;
@@ -163,7 +163,7 @@ void* HipDevice::scratch(size_t bytes, int slot) {
   if (bytes > scratch_sz_[slot]) {
     activate();
     sync_all();
-    if (scratch_[slot]) hipFree(scratch_[slot]);
+    if (scratch_[slot]) (void)hipFree(scratch_[slot]);
     scratch_[slot] = nullptr;
     HIP_OK(hipMalloc(&scratch_[slot], bytes));
     scratch_sz_[slot] = bytes;

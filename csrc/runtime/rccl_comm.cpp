@@ -35,7 +35,7 @@ std::string RcclComm::unique_id() {
 RcclComm::RcclComm(const std::vector<std::string>& ids, int nranks, int rank, int device)
     : n_(nranks), r_(rank), device_(device) {
   GJ_REQUIRE(ids.size() == 2, "RcclComm needs two unique ids");
-  hipSetDevice(device_);
+  (void)hipSetDevice(device_);
   for (int c = 0; c < 2; ++c) {
     GJ_REQUIRE(ids[c].size() == sizeof(ncclUniqueId), "bad unique id size");
     ncclUniqueId id;
@@ -49,10 +49,10 @@ RcclComm::RcclComm(const std::vector<std::string>& ids, int nranks, int rank, in
 }
 
 RcclComm::~RcclComm() {
-  hipSetDevice(device_);
+  (void)hipSetDevice(device_);
   for (void* c : comms_)
     if (c) ncclCommDestroy(static_cast<ncclComm_t>(c));
-  if (dbuf_) hipFree(dbuf_);
+  if (dbuf_) (void)hipFree(dbuf_);
 }
 
 std::string RcclComm::describe() const {
@@ -105,7 +105,7 @@ void RcclComm::check_health() {
 }
 
 void RcclComm::abort() {
-  hipSetDevice(device_);
+  (void)hipSetDevice(device_);
   for (void*& c : comms_)
     if (c) {
       ncclCommAbort(static_cast<ncclComm_t>(c));
@@ -120,7 +120,7 @@ void RcclComm::barrier(Device& dev) {
 }
 
 double RcclComm::host_max(Device& dev, double v) {
-  hipSetDevice(device_);
+  (void)hipSetDevice(device_);
   dev.sync_stream(S_SIDE);
   double* d = static_cast<double*>(dbuf_);
   dev.copy(d, &v, sizeof(double), S_SIDE);
@@ -132,7 +132,7 @@ double RcclComm::host_max(Device& dev, double v) {
 }
 
 void RcclComm::host_allgather(Device& dev, const void* send, void* recv, size_t bytes) {
-  hipSetDevice(device_);
+  (void)hipSetDevice(device_);
   const size_t need = bytes * (n_ + 1);
   void* tmp = dbuf_;
   bool owned = false;
@@ -146,7 +146,7 @@ void RcclComm::host_allgather(Device& dev, const void* send, void* recv, size_t 
   allgather(dev, d, d + bytes, bytes, S_SIDE);
   dev.copy(recv, d + bytes, bytes * n_, S_SIDE);
   dev.sync_stream(S_SIDE);
-  if (owned) hipFree(tmp);
+  if (owned) (void)hipFree(tmp);
 }
 
 }  // namespace gj

@@ -35,9 +35,9 @@ void rank_main(const RunConfig& cfg, int rank, Shared& sh, std::shared_ptr<Loopb
   std::unique_ptr<Comm> comm;
   if (cfg.gpu) {
     int ndev = 0;
-    hipGetDeviceCount(&ndev);
+    (void)hipGetDeviceCount(&ndev);
     const int d = (cfg.first_device + rank) % std::max(ndev, 1);
-    hipSetDevice(d);
+    (void)hipSetDevice(d);
     dev.reset(new HipDevice(d));
     if (use_rccl)
       comm.reset(new RcclComm(ids, cfg.ranks, rank, d));
