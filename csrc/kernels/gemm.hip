@@ -28,6 +28,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 
 #include "kernels.hpp"
 
@@ -35,13 +36,19 @@ namespace gj {
 namespace kern {
 
 constexpr int PADL = 16;                          // LDS row pad (elements): conflict-free frag reads
-constexpr int kRecords = 0x7ffffff0;              // buffer extent; every access is masked explicitly
+constexpr int kRecords = 0x7ffffff0;              // buffer extent of every resource
+// Masked-off lanes use this per-lane offset (>= kRecords): the buffer unit returns 0 for such a load
+// and drops such a store, so no access needs a branch.  Branch-free loads matter: a load behind a
+// per-lane condition makes hipcc wait vmcnt(0) at the next use of ANY load result, which drains the
+// K-slice prefetch every iteration.
+constexpr int kOOB = 0x7ffffff8;
 
 // Tile configurations.  WM x WN waves, each owning a (BM/WM) x (BN/WN) block of 16x16 MFMA tiles.
 // OCC = workgroups per CU the launch bounds are written for.
-template <int BM_, int BN_, int BK_, int WM_, int WN_, int OCC_>
+template <int BM_, int BN_, int BK_, int WM_, int WN_, int OCC_, int PF_ = 1>
 struct Cfg {
   static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_, WN = WN_, OCC = OCC_;
+  static constexpr int PF = PF_;  // K slices in flight in registers (1 or 2) ahead of the LDS slice
   static constexpr int NT = 64 * WM * WN;
   static constexpr int TM = BM / WM, TN = BN / WN;
   static constexpr int MI = TM / 16, NJ = TN / 16;
@@ -55,6 +62,13 @@ using CfgBig = Cfg<128, 128, 16, 2, 4, 2>;   // 512 threads, 2 WG/CU (73.7 KiB L
 using CfgNarrow = Cfg<128, 64, 8, 2, 2, 4>;  // 256 threads, 4 WG/CU (28.7 KiB LDS each)
 using CfgTall = Cfg<64, 128, 8, 1, 4, 4>;    // 256 threads, 4 WG/CU
 using CfgSmall = Cfg<64, 32, 16, 2, 1, 8>;   // 128 threads: latency-bound panel GEMMs (few tiles)
+// tuning candidates (GJ_GEMM_VARIANT)
+using CfgNarrowPf = Cfg<128, 64, 8, 2, 2, 3, 2>;  // narrow, two register stages in flight
+using CfgSquare = Cfg<128, 128, 8, 2, 2, 2>;      // 256 threads, 64x64 per wave (16 MFMA tiles)
+using CfgSquarePf = Cfg<128, 128, 8, 2, 2, 2, 2>;
+using CfgWide = Cfg<256, 128, 8, 4, 2, 1, 2>;     // 512 threads, 64x64 per wave
+using CfgBig8 = Cfg<128, 128, 8, 2, 4, 2, 2>;     // big tile, BK 8, two stages
+using CfgBigPf = Cfg<128, 128, 16, 2, 4, 2, 2>;
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
@@ -105,7 +119,6 @@ __device__ __forceinline__ void bstore(float v, __amdgpu_buffer_rsrc_t r, int vo
 }
 
 enum { MODE_ACC = 0, MODE_STORE = 1, MODE_RESID = 2 };
-
 struct GemmArgs {
   int64_t M, N, K;
   const void* A;
@@ -124,6 +137,7 @@ struct GemmArgs {
   double* partial;  // [M][nparts]
   int nparts;
   bool latency;     // GemmExtra::latency -> CfgSmall for few-tile launches
+  int ablate;       // timing probe only (GJ_GEMM_ABLATE=1): no K-slice staging inside the loop
 };
 
 // XCD-aware bijective remap: blocks b and b+8 share an XCD (MI355X_MICROARCH.md §Workgroup
@@ -189,7 +203,7 @@ __global__ __launch_bounds__(CF::NT, CF::WAVES_PER_SIMD) void gemm_kernel(GemmAr
         for (int j = 0; j < NJ; ++j) {
           const int c = clane + j * 16;
           const bool ok = r < Mt && c < Nt && !zrow && !(c >= z0 && c < z1);
-          acc[i][j][q] = ok ? bload<T>(rc, cvoff + j * 16 * ES, soff) : T(0);
+          acc[i][j][q] = bload<T>(rc, ok ? cvoff + j * 16 * ES : kOOB, soff);
         }
       }
   } else {
@@ -209,21 +223,23 @@ __global__ __launch_bounds__(CF::NT, CF::WAVES_PER_SIMD) void gemm_kernel(GemmAr
   const bool a_col_ok = (m0 + am_l) < g.M;
   const int b_voff = (bk_l * ldb + bn_l) * ES;
   const int a_voff = (AL == 1) ? (ak_l * lda + am_l) * ES : 0;
-  T ra[CF::SPA], rb[CF::SPB];
-  auto load_slice = [&](int64_t k0) {
+  T ra[CF::PF][CF::SPA], rb[CF::PF][CF::SPB];
+  // column masks folded into the per-lane offsets once; the K bound is a 32-bit compare against
+  // the (scalar) rows left in the slice, so the staging needs no 64-bit temporaries
+  const int b_vo = b_col_ok ? b_voff : kOOB;
+  const int a_vo = a_col_ok ? a_voff : kOOB;
+  auto load_slice = [&](int64_t k0, auto slot) {
+    constexpr int S = decltype(slot)::value;
+    const int krem = (int)((g.K - k0) < BK ? (g.K - k0) : BK);
     __amdgpu_buffer_rsrc_t rbr = rsrc(B + k0 * g.ldb + n0);
 #pragma unroll
-    for (int e = 0; e < CF::SPB; ++e) {
-      const int64_t gk = k0 + e * KPB + bk_l;
-      rb[e] = (gk < g.K && b_col_ok) ? bload<T>(rbr, b_voff, e * KPB * ldb * ES) : T(0);
-    }
+    for (int e = 0; e < CF::SPB; ++e)
+      rb[S][e] = bload<T>(rbr, (e * KPB + bk_l < krem) ? b_vo : kOOB, e * KPB * ldb * ES);
     if (AL == 1) {
       __amdgpu_buffer_rsrc_t rar = rsrc(A + k0 * g.lda + m0);
 #pragma unroll
-      for (int e = 0; e < CF::SPA; ++e) {
-        const int64_t gk = k0 + e * KPA + ak_l;
-        ra[e] = (gk < g.K && a_col_ok) ? bload<T>(rar, a_voff, e * KPA * lda * ES) : T(0);
-      }
+      for (int e = 0; e < CF::SPA; ++e)
+        ra[S][e] = bload<T>(rar, (e * KPA + ak_l < krem) ? a_vo : kOOB, e * KPA * lda * ES);
     } else {
       __amdgpu_buffer_rsrc_t rar = rsrc(A + m0 * g.lda + k0);
 #pragma unroll
@@ -231,31 +247,25 @@ __global__ __launch_bounds__(CF::NT, CF::WAVES_PER_SIMD) void gemm_kernel(GemmAr
         const int idx = e * NT + tid;
         const int ii = idx / BK, kk = idx % BK;
         const bool ok = (k0 + kk) < g.K && (m0 + ii) < g.M;
-        ra[e] = ok ? bload<T>(rar, (ii * lda + kk) * ES, 0) : T(0);
+        ra[S][e] = bload<T>(rar, ok ? (ii * lda + kk) * ES : kOOB, 0);
       }
     }
   };
-  auto store_slice = [&](int buf) {
+  auto store_slice = [&](int buf, auto slot) {
+    constexpr int S = decltype(slot)::value;
 #pragma unroll
-    for (int e = 0; e < CF::SPB; ++e) ldsB[buf][e * KPB + bk_l][bn_l] = rb[e];
+    for (int e = 0; e < CF::SPB; ++e) ldsB[buf][e * KPB + bk_l][bn_l] = rb[S][e];
 #pragma unroll
     for (int e = 0; e < CF::SPA; ++e) {
       if (AL == 1) {
-        ldsA[buf][e * KPA + ak_l][am_l] = ra[e];
+        ldsA[buf][e * KPA + ak_l][am_l] = ra[S][e];
       } else {
         const int idx = e * NT + tid;
-        ldsA[buf][idx % BK][idx / BK] = ra[e];
+        ldsA[buf][idx % BK][idx / BK] = ra[S][e];
       }
     }
   };
-
-  const int nk = (int)((g.K + BK - 1) / BK);
-  load_slice(0);
-  store_slice(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) load_slice((int64_t)(kt + 1) * BK);
+  auto compute = [&](int cur) {
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
       T a[MI], b[NJ];
@@ -269,8 +279,45 @@ __global__ __launch_bounds__(CF::NT, CF::WAVES_PER_SIMD) void gemm_kernel(GemmAr
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = MF::op(a[i], b[j], acc[i][j]);
     }
-    if (kt + 1 < nk) store_slice(cur ^ 1);
-    __syncthreads();
+  };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, (CF::PF > 1 ? 1 : 0)>;
+
+  const int nk = (int)((g.K + BK - 1) / BK);
+  load_slice(0, S0{});
+  store_slice(0, S0{});
+  // The C loads were issued before slice 0, so they are complete here; say so to the compiler:
+  // otherwise the accumulators' pending loads merge into the loop header and hipcc waits vmcnt(0)
+  // inside every iteration, draining the prefetch of the next K slice.
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) asm volatile("" ::"v"(acc[i][j][q]));
+  if (CF::PF > 1 && nk > 1) load_slice((int64_t)BK, S1{});
+  __syncthreads();
+  if (CF::PF == 1) {
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk && !g.ablate) load_slice((int64_t)(kt + 1) * BK, S0{});
+      compute(cur);
+      if (kt + 1 < nk && !g.ablate) store_slice(cur ^ 1, S0{});
+      __syncthreads();
+    }
+  } else {
+    // slice s lives in register slot s & 1: slice kt+2 is fetched while slice kt is multiplied
+    // and slice kt+1 (fetched one iteration earlier) is written to the other LDS buffer.
+    auto body = [&](int kt, auto ld_slot, auto st_slot) {
+      if (kt + 2 < nk && !g.ablate) load_slice((int64_t)(kt + 2) * BK, ld_slot);
+      compute(kt & 1);
+      if (kt + 1 < nk && !g.ablate) store_slice((kt & 1) ^ 1, st_slot);
+      __syncthreads();
+    };
+    for (int kt = 0; kt < nk; kt += 2) {
+      body(kt, S0{}, S1{});
+      if (kt + 1 < nk) body(kt + 1, S1{}, S0{});
+    }
   }
 
   if (MODE == MODE_ACC || MODE == MODE_STORE) {
@@ -283,7 +330,7 @@ __global__ __launch_bounds__(CF::NT, CF::WAVES_PER_SIMD) void gemm_kernel(GemmAr
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const int c = clane + j * 16;
-          if (r < Mt && c < Nt) bstore(acc[i][j][q], rc, cvoff + j * 16 * ES, soff);
+          bstore(acc[i][j][q], rc, (r < Mt && c < Nt) ? cvoff + j * 16 * ES : kOOB, soff);
         }
       }
   } else {  // MODE_RESID: per-row partial sum of |acc - I| over this wave's TN real columns
@@ -317,18 +364,23 @@ static void launch_cfg(const GemmArgs& a0, hipStream_t s) {
   hipLaunchKernelGGL((gemm_kernel<T, AL, MODE, CF>), dim3((unsigned)nwg), dim3(CF::NT), 0, s, a);
 }
 
-// Variant selection (GJ_GEMM_VARIANT=big|narrow|tall or set_gemm_variant(); default by measurement).
+// Variant selection (GJ_GEMM_VARIANT=<name> or set_gemm_variant(); default "auto": per shape, by
+// measurement — profiles/gemm_variants_k512.jsonl).
+constexpr int kAutoVariant = 10;
 static int g_variant = -1;
 static int gemm_variant() {
   if (g_variant < 0) {
     const char* e = getenv("GJ_GEMM_VARIANT");
-    g_variant = e ? gemm_variant_id(e) : 1;  // narrow: 4 WG/CU hides C latency best (bench_gemm)
+    g_variant = e ? gemm_variant_id(e) : kAutoVariant;
   }
   return g_variant;
 }
 int gemm_variant_id(const char* name) {
   const std::string s(name);
-  return s == "big" ? 0 : s == "tall" ? 2 : s == "valu" ? 3 : 1;
+  static const char* names[] = {"big", "narrow", "tall", "valu", "narrowpf", "square", "squarepf", "wide", "big8", "bigpf", "auto"};
+  for (int i = 0; i < (int)(sizeof(names) / sizeof(names[0])); ++i)
+    if (s == names[i]) return i;
+  return kAutoVariant;
 }
 void set_gemm_variant(int v) { g_variant = v; }
 
@@ -342,10 +394,25 @@ static void launch(const GemmArgs& a, hipStream_t s) {
   const int64_t narrow_tiles = ((a.M + CfgNarrow::BM - 1) / CfgNarrow::BM) * ((a.N + CfgNarrow::BN - 1) / CfgNarrow::BN);
   if (a.latency && narrow_tiles < kSmallGridTiles && gemm_variant() != 0)
     return launch_cfg<T, AL, MODE, CfgSmall>(a, s);
-  switch (gemm_variant()) {
+  int v = gemm_variant();
+  if (v == kAutoVariant) {
+    // Deep trailing updates (K >= 384) with enough 128x128 tiles to fill the chip: the big tile with
+    // two K slices in flight (fp64 57.6 vs 53.5 TF narrow at 32768x4096x512; fp32 the 64x64-per-wave
+    // square tile, 106.6 vs 97.5 TF).  Everything else keeps the 4-WG/CU narrow tile.
+    const int64_t big_tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
+    const bool deep = a.K >= 384 && big_tiles >= 512;
+    v = !deep ? 1 : (sizeof(T) == 8 ? 9 : 6);
+  }
+  switch (v) {
     case 1: return launch_cfg<T, AL, MODE, CfgNarrow>(a, s);
     case 2: return launch_cfg<T, AL, MODE, CfgTall>(a, s);
     case 3: return launch_cfg<T, AL, MODE, CfgNarrow>(a, s);  // valu is fp64/K-major only
+    case 4: return launch_cfg<T, AL, MODE, CfgNarrowPf>(a, s);
+    case 5: return launch_cfg<T, AL, MODE, CfgSquare>(a, s);
+    case 6: return launch_cfg<T, AL, MODE, CfgSquarePf>(a, s);
+    case 7: return launch_cfg<T, AL, MODE, CfgWide>(a, s);
+    case 8: return launch_cfg<T, AL, MODE, CfgBig8>(a, s);
+    case 9: return launch_cfg<T, AL, MODE, CfgBigPf>(a, s);
     default: return launch_cfg<T, AL, MODE, CfgBig>(a, s);
   }
 }
@@ -357,6 +424,8 @@ static void fill_extra(GemmArgs& a, const GemmExtra* ex) {
   a.zh = ex ? ex->zh : 0;
   for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) a.zr[z] = (ex && z < ex->nzr) ? ex->zr[z] : kNone;
   a.latency = ex ? ex->latency : false;
+  static const int ablate = getenv("GJ_GEMM_ABLATE") ? atoi(getenv("GJ_GEMM_ABLATE")) : 0;
+  a.ablate = ablate;
 }
 
 void gemm(DType dt, int op, int a_kmajor, int64_t M, int64_t N, int64_t K, const void* A,

@@ -124,10 +124,17 @@ def test_row_abs_max_and_residual():
     assert r < 1e-10 and abs(r - ref) < 1e-11
 
 
-@pytest.mark.parametrize("variant", ["big", "narrow", "tall", "valu"])
-@pytest.mark.parametrize("M,N,K", [(256, 384, 128), (300, 200, 60), (1000, 130, 256), (2100, 1600, 136)])
-def test_gemm_variants_elimination_extras(native, variant, M, N, K):
+GEMM_VARIANTS = ["big", "narrow", "tall", "valu", "narrowpf", "square", "squarepf", "wide", "big8", "bigpf", "auto"]
+
+
+@pytest.mark.parametrize("variant", GEMM_VARIANTS)
+@pytest.mark.parametrize("M,N,K", [(256, 384, 128), (300, 200, 60), (1000, 130, 256), (2100, 1600, 136),
+                                   (700, 1100, 512), (1536, 1024, 520)])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_gemm_variants_elimination_extras(native, variant, M, N, K, dtype):
     """All kernel variants: C += A B where C enters as 0 in a column range and in two row blocks."""
+    if variant == "valu" and dtype == torch.float32:
+        pytest.skip("the VALU variant is fp64-only")
     native.set_gemm_variant(variant)
     try:
         A = _rand((M, K), torch.float64, 11)
@@ -139,12 +146,13 @@ def test_gemm_variants_elimination_extras(native, variant, M, N, K):
         for r in zr:
             Cin[r:r + zh] = 0
         ref = Cin + A @ B
-        Cd = C.cuda()
-        ops.gemm(A.t().contiguous().cuda(), B.cuda(), Cd, op="acc", a_kmajor=True, zero_cols=(z0, z1),
-                 zero_rows=zr, zero_row_height=zh)
-        assert (Cd.cpu() - ref).abs().max().item() < 1e-12 * K
-        Cs = torch.zeros(M, N, dtype=torch.float64).cuda()
-        ops.gemm(A.t().contiguous().cuda(), B.cuda(), Cs, op="store", a_kmajor=True)
-        assert (Cs.cpu() - A @ B).abs().max().item() < 1e-12 * K
+        tol = (1e-12 if dtype == torch.float64 else 2e-5) * K
+        Cd = C.to(dtype).cuda()
+        ops.gemm(A.t().contiguous().to(dtype).cuda(), B.to(dtype).cuda(), Cd, op="acc", a_kmajor=True,
+                 zero_cols=(z0, z1), zero_rows=zr, zero_row_height=zh)
+        assert (Cd.cpu().double() - ref).abs().max().item() < tol
+        Cs = torch.zeros(M, N, dtype=dtype).cuda()
+        ops.gemm(A.t().contiguous().to(dtype).cuda(), B.to(dtype).cuda(), Cs, op="store", a_kmajor=True)
+        assert (Cs.cpu().double() - A @ B).abs().max().item() < tol
     finally:
-        native.set_gemm_variant("narrow")
+        native.set_gemm_variant("auto")
