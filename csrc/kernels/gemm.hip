@@ -138,6 +138,7 @@ struct GemmArgs {
   int nparts;
   bool latency;     // GemmExtra::latency -> CfgSmall for few-tile launches
   int ablate;       // timing probe only (GJ_GEMM_ABLATE=1): no K-slice staging inside the loop
+  int group;        // LDS-DMA kernel: tile rows per column-walk group (1 = row-major tile order)
 };
 
 // XCD-aware bijective remap: blocks b and b+8 share an XCD (MI355X_MICROARCH.md §Workgroup
@@ -354,6 +355,211 @@ __global__ __launch_bounds__(CF::NT, CF::WAVES_PER_SIMD) void gemm_kernel(GemmAr
   }
 }
 
+// ---- fp64 trailing-update GEMM with LDS-DMA staging (buffer_load_dwordx4 ... lds).
+//
+// Same tile as CfgNarrow (128 x 64 per 256-thread workgroup, 2 x 2 waves of 64 x 32) but the K
+// slices go global -> LDS without registers: each wave issues three 1-KiB LDS-DMA pieces per
+// 8-deep slice (two A rows, then two B rows) into an NS-stage LDS ring, and the only waits in the
+// loop are a counted vmcnt and a raw s_barrier.  Freeing the staging registers lets five
+// workgroups share a CU.  Measured at 32768 x 4096 x 512: 62.6 TF/s (register staging 57.6; the
+// same tile with no staging at all — GJ_GEMM_ABLATE — 66.8).  Masked elements come back as zeros
+// from out-of-range buffer offsets.
+// LDS images: A [k][128 + 16 pad] (one DMA piece = one k row); B [k][64] with the two 128-B halves
+// of every odd row swapped (element n of row k at n ^ 16(k&1)), so the four k rows read by one
+// ds_read_b64 land on distinct bank halves; the swizzle is applied to the global source address.
+// Requirements (checked by the dispatcher): K-major A, M, N, lda, ldb even, A/B 16-byte aligned.
+namespace glds {
+constexpr int BM = 128, BN = 64, BK = 8, NT = 256;
+constexpr int LDA = BM + 16;                 // A row stride (doubles)
+constexpr int SA = BK * LDA, SB = BK * BN;   // stage sizes (doubles)
+constexpr int STAGE = SA + SB;
+}  // namespace glds
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, double* lds_wave_base, int voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16,
+                                           voff, 0, 0, 0);
+}
+
+// s_waitcnt vmcnt(3 * n) for a runtime n <= 3 (the pieces of n slices may stay in flight)
+__device__ __forceinline__ void wait_pieces(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+  }
+}
+
+template <int MODE, int NS, int OCC>
+__global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
+  using namespace glds;
+  static_assert(NS >= 2 && NS <= 5, "stages");
+  using MF = Mfma<double>;
+  using acc_t = MF::acc_t;
+  constexpr int ES = 8, TM = 64, TN = 32, MI = 4, NJ = 2, WN = 2;
+  __shared__ double lds[NS * STAGE];
+
+  const int nwg = g.tiles_m * g.tiles_n;
+  const int tile = xcd_remap((int)blockIdx.x, nwg);
+  // groups of G tile rows walked column by column: the tiles in flight on one XCD then share
+  // G A-slabs and a narrow band of B instead of all of B
+  const int G = g.group > 0 ? g.group : 1;
+  const int grp = tile / (G * g.tiles_n), gr0 = grp * G;
+  const int gsz = (g.tiles_m - gr0) < G ? (g.tiles_m - gr0) : G;
+  const int rem = tile - grp * G * g.tiles_n;
+  const int tm = gr0 + rem % gsz, tn = rem / gsz;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const double* A = static_cast<const double*>(g.A);
+  const double* B = static_cast<const double*>(g.B);
+  double* C = static_cast<double*>(g.C);
+  const int ldc = (int)g.ldc, ldb = (int)g.ldb, lda = (int)g.lda;
+
+  const int rlane = wm * TM + MF::rl(lane);
+  const int clane = wn * TN + (lane & 15);
+  const int Mt = (int)((g.M - m0) < BM ? (g.M - m0) : BM);
+  const int Nt = (int)((g.N - n0) < BN ? (g.N - n0) : BN);
+  const int64_t zlo = g.zc0 - n0, zhi = g.zc1 - n0;
+  const int z0 = (int)(zlo < 0 ? 0 : (zlo > BN ? BN : zlo)), z1 = (int)(zhi < 0 ? 0 : (zhi > BN ? BN : zhi));
+  int zr0[GemmExtra::kMaxZeroRows], zr1[GemmExtra::kMaxZeroRows];
+#pragma unroll
+  for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) {
+    const int64_t lo = g.zr[z] - m0, hi = g.zr[z] + g.zh - m0;
+    zr0[z] = (int)(lo < 0 ? 0 : (lo > BM ? BM : lo));
+    zr1[z] = (int)(hi < 0 ? 0 : (hi > BM ? BM : hi));
+  }
+  __amdgpu_buffer_rsrc_t rc = rsrc(C + m0 * g.ldc + n0);
+  const int cvoff = (rlane * ldc + clane) * ES;
+
+  acc_t acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = rlane + i * 16 + MF::rq(q);
+      const int soff = (i * 16 + MF::rq(q)) * ldc * ES;
+      bool zrow = false;
+#pragma unroll
+      for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) zrow |= (r >= zr0[z] && r < zr1[z]);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int c = clane + j * 16;
+        if (MODE == MODE_ACC) {
+          const bool ok = r < Mt && c < Nt && !zrow && !(c >= z0 && c < z1);
+          acc[i][j][q] = bload<double>(rc, ok ? cvoff + j * 16 * ES : kOOB, soff);
+        } else {
+          acc[i][j][q] = 0.0;
+        }
+      }
+    }
+  // C must have landed before the first LDS-DMA is counted by the hand-written waits below
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) asm volatile("" ::"v"(acc[i][j][q]));
+
+  // DMA piece geometry (per wave, per slice): A rows wid and wid + 4 (lane l -> columns 2l, 2l+1);
+  // B rows 2 wid + (l >> 5), columns 2 (l & 31) of the swizzled image.
+  const int acol = 2 * lane;
+  const bool a_ok = (m0 + acol) < g.M;
+  const int brow = 2 * wid + (lane >> 5);
+  const int bpos = 2 * (lane & 31);
+  const int bcol = bpos ^ ((brow & 1) * 16);
+  const bool b_ok = (n0 + bcol) < g.N;
+  __amdgpu_buffer_rsrc_t ra = rsrc(A + m0);
+  __amdgpu_buffer_rsrc_t rb = rsrc(B + n0);
+  const int Kd = (int)g.K;
+  auto issue = [&](int kt) {
+    double* st = lds + (kt % NS) * STAGE;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int kr = wid + 4 * h;
+      const bool ok = a_ok && (k0 + kr) < Kd;
+      dma16(ra, st + kr * LDA, ok ? ((k0 + kr) * lda + acol) * ES : kOOB);
+    }
+    const bool okb = b_ok && (k0 + brow) < Kd;
+    dma16(rb, st + SA + 2 * wid * BN, okb ? ((k0 + brow) * ldb + bcol) * ES : kOOB);
+  };
+  auto compute = [&](int kt) {
+    const double* sa = lds + (kt % NS) * STAGE;
+    const double* sb = sa + SA;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 4) {
+      double a[MI], b[NJ];
+      const int kr = kk + (lane >> 4);
+      const int sw = (kr & 1) * 16;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a[i] = sa[kr * LDA + wm * TM + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) b[j] = sb[kr * BN + ((wn * TN + j * 16 + (lane & 15)) ^ sw)];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = MF::op(a[i], b[j], acc[i][j]);
+    }
+  };
+
+  const int nk = (int)((g.K + BK - 1) / BK);
+  const int pro = nk < NS - 1 ? nk : NS - 1;  // slices issued ahead
+  for (int kt = 0; kt < pro; ++kt) issue(kt);
+  wait_pieces(pro - 1);  // slice 0 landed
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + NS - 1 < nk) issue(kt + NS - 1);
+    compute(kt);
+    // slice kt+1 must have landed (this wave's pieces); the later issued ones may stay in flight
+    const int last = (kt + NS - 1 < nk ? kt + NS - 1 : nk - 1);
+    wait_pieces(last - (kt + 1) > 0 ? last - (kt + 1) : 0);
+    __builtin_amdgcn_s_barrier();
+  }
+
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = rlane + i * 16 + MF::rq(q);
+      const int soff = (i * 16 + MF::rq(q)) * ldc * ES;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int c = clane + j * 16;
+        bstore(acc[i][j][q], rc, (r < Mt && c < Nt) ? cvoff + j * 16 * ES : kOOB, soff);
+      }
+    }
+}
+
+template <int MODE>
+static void launch_glds(const GemmArgs& a0, hipStream_t s) {
+  GemmArgs a = a0;
+  a.tiles_m = (int)((a.M + glds::BM - 1) / glds::BM);
+  a.tiles_n = (int)((a.N + glds::BN - 1) / glds::BN);
+  const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;
+  if (nwg <= 0) return;
+  // default (measured, 32768 x 4096 x 512): 2 stages at 5 workgroups per CU, groups of 4 tile rows
+  // = 62.6 TF/s; 3/4/5 stages at 4/3/2 WG/CU: 59.4/59.1/53.7; 2 stages at 4 WG/CU: 61.2
+  static const int stages = getenv("GJ_GLDS_STAGES") ? atoi(getenv("GJ_GLDS_STAGES")) : 6;
+  static const int group = getenv("GJ_GEMM_GROUP") ? atoi(getenv("GJ_GEMM_GROUP")) : 4;
+  a.group = group;
+  const dim3 grid((unsigned)nwg), blk(glds::NT);
+  switch (stages) {  // LDS per workgroup: 13.3 KiB per stage
+    case 2: hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 4>), grid, blk, 0, s, a); break;
+    case 6: hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 5>), grid, blk, 0, s, a); break;  // 2 stages, 5 WG/CU
+    case 4: hipLaunchKernelGGL((gemm_glds_f64<MODE, 4, 3>), grid, blk, 0, s, a); break;
+    case 5: hipLaunchKernelGGL((gemm_glds_f64<MODE, 5, 2>), grid, blk, 0, s, a); break;
+    default: hipLaunchKernelGGL((gemm_glds_f64<MODE, 3, 4>), grid, blk, 0, s, a); break;
+  }
+}
+
+static bool glds_ok(const GemmArgs& a) {
+  const auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  return a.M % 2 == 0 && a.N % 2 == 0 && a.lda % 2 == 0 && a.ldb % 2 == 0 && al16(a.A) && al16(a.B) &&
+         a.lda * a.K * 8 < kRecords && a.ldb * a.K * 8 < kRecords && a.ldc * 128 * 8 < kRecords;
+}
+
 template <typename T, int AL, int MODE, typename CF>
 static void launch_cfg(const GemmArgs& a0, hipStream_t s) {
   GemmArgs a = a0;
@@ -377,7 +583,7 @@ static int gemm_variant() {
 }
 int gemm_variant_id(const char* name) {
   const std::string s(name);
-  static const char* names[] = {"big", "narrow", "tall", "valu", "narrowpf", "square", "squarepf", "wide", "big8", "bigpf", "auto"};
+  static const char* names[] = {"big", "narrow", "tall", "valu", "narrowpf", "square", "squarepf", "wide", "big8", "bigpf", "auto", "glds"};
   for (int i = 0; i < (int)(sizeof(names) / sizeof(names[0])); ++i)
     if (s == names[i]) return i;
   return kAutoVariant;
@@ -401,7 +607,13 @@ static void launch(const GemmArgs& a, hipStream_t s) {
     // square tile, 106.6 vs 97.5 TF).  Everything else keeps the 4-WG/CU narrow tile.
     const int64_t big_tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
     const bool deep = a.K >= 384 && big_tiles >= 512;
-    v = !deep ? 1 : (sizeof(T) == 8 ? 9 : 6);
+    v = !deep ? 1 : (sizeof(T) == 8 ? 11 : 6);
+  }
+  if (v == 11) {  // LDS-DMA fp64 kernel; other dtypes / layouts / alignments take the next best tile
+    if constexpr (sizeof(T) == 8 && AL == 1 && MODE != MODE_RESID) {
+      if (glds_ok(a)) return launch_glds<MODE>(a, s);
+    }
+    v = sizeof(T) == 8 ? 9 : 6;
   }
   switch (v) {
     case 1: return launch_cfg<T, AL, MODE, CfgNarrow>(a, s);

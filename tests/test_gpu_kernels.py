@@ -124,7 +124,7 @@ def test_row_abs_max_and_residual():
     assert r < 1e-10 and abs(r - ref) < 1e-11
 
 
-GEMM_VARIANTS = ["big", "narrow", "tall", "valu", "narrowpf", "square", "squarepf", "wide", "big8", "bigpf", "auto"]
+GEMM_VARIANTS = ["big", "narrow", "tall", "valu", "narrowpf", "square", "squarepf", "wide", "big8", "bigpf", "auto", "glds"]
 
 
 @pytest.mark.parametrize("variant", GEMM_VARIANTS)
