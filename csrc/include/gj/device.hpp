@@ -35,10 +35,10 @@ enum class ALayout : int { RowMajor = 0, KMajor = 1 };
 // Elimination extras of GemmOp::Acc: C enters as 0 in the columns [zc0, zc1) (the pivot block
 // columns of the current panel) and in the row blocks [zr[i], zr[i] + zh) (its pivot rows).
 struct GemmExtra {
-  static constexpr int kMaxZeroRows = 4;
+  static constexpr int kMaxZeroRows = 8;  // = the deepest panel (SolveOptions::depth <= 8)
   int64_t zc0 = 0, zc1 = 0;
   int nzr = 0;
-  int64_t zr[kMaxZeroRows] = {0, 0, 0, 0};
+  int64_t zr[kMaxZeroRows] = {};
   int64_t zh = 0;
   // Few-tile GEMM on the panel-factorisation critical path: prefer small tiles (more workgroups,
   // shorter K loop per workgroup) over the throughput tiles of the trailing update.

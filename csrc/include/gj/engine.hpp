@@ -38,7 +38,7 @@ namespace gj {
 struct SolveOptions {
   DType dtype = DType::F64;
   int64_t chunk_cols = 0;   // pipelining granularity of the pivot-row broadcast (0 = auto)
-  int depth = 4;            // elimination steps fused per trailing update (K = depth*m), 1..4
+  int depth = 4;            // elimination steps fused per trailing update (K = depth*m), 1..8
   double eps = kDefaultEps;
   bool sync_debug = false;  // synchronise every stream after every phase (race screening)
   bool profile = false;     // per-phase device timers (HIP events) + roctx ranges

@@ -539,9 +539,12 @@ static void launch_glds(const GemmArgs& a0, hipStream_t s) {
   a.tiles_n = (int)((a.N + glds::BN - 1) / glds::BN);
   const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;
   if (nwg <= 0) return;
-  // default (measured, 32768 x 4096 x 512): 2 stages at 5 workgroups per CU, groups of 4 tile rows
-  // = 62.6 TF/s; 3/4/5 stages at 4/3/2 WG/CU: 59.4/59.1/53.7; 2 stages at 4 WG/CU: 61.2
-  static const int stages = getenv("GJ_GLDS_STAGES") ? atoi(getenv("GJ_GLDS_STAGES")) : 6;
+  // Pipeline depth / occupancy, measured at 32768 x 4096 x 512 alone: 2 stages at 5 WG/CU ("6")
+  // 62.6 TF/s, at 4 WG/CU 61.2; 3/4/5 stages at 4/3/2 WG/CU 59.4/59.1/53.7.  Inside the solver the
+  // 4-WG/CU form wins (N=32768: 1155 vs 1205 ms, profiles/cu_reserve_sweep.md): the register/LDS
+  // room it leaves lets the latency-bound pivot-path kernels start without waiting for the GEMM
+  // to drain.  Tile rows are walked in groups of 4 (+0.5-1 %).
+  static const int stages = getenv("GJ_GLDS_STAGES") ? atoi(getenv("GJ_GLDS_STAGES")) : 2;
   static const int group = getenv("GJ_GEMM_GROUP") ? atoi(getenv("GJ_GEMM_GROUP")) : 4;
   a.group = group;
   const dim3 grid((unsigned)nwg), blk(glds::NT);

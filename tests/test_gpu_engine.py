@@ -10,7 +10,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("n,m", [(1000, 128), (517, 60), (64, 64), (300, 256), (10, 12), (40, 1)])
 @pytest.mark.parametrize("gen", ["random", "absdiff"])
-@pytest.mark.parametrize("depth", [1, 2, 3, 4])
+@pytest.mark.parametrize("depth", [1, 2, 3, 4, 8])
 def test_engine_single_gpu_vs_numpy(native, n, m, gen, depth):
     eng = native.Engine(native.hip_device(0), native.self_comm(), n, m, "fp64", 0, 1e-15, False, depth)
     eng.generate(gen, 5)
@@ -26,7 +26,7 @@ def test_engine_single_gpu_vs_numpy(native, n, m, gen, depth):
 
 
 @pytest.mark.parametrize("p", [2, 3, 4])
-@pytest.mark.parametrize("depth", [1, 2])
+@pytest.mark.parametrize("depth", [1, 2, 8])
 def test_loopback_ranks_on_one_gpu(p, depth):
     n, m = 700, 64
     A = generate_matrix(n, "random", 9)

@@ -116,7 +116,7 @@ def test_solve_rhs():
     assert np.abs(got - x).max() < 1e-9
 
 
-@pytest.mark.parametrize("depth", [1, 2, 3, 4])
+@pytest.mark.parametrize("depth", [1, 2, 3, 4, 6, 8])
 @pytest.mark.parametrize("n,m,p", [(37, 5, 1), (37, 5, 3), (64, 8, 2), (10, 3, 4), (50, 7, 5), (12, 12, 2)])
 @pytest.mark.parametrize("kind", ["rand", "perm"])
 def test_depth_variants_match_numpy(depth, n, m, p, kind):
