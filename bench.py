@@ -43,6 +43,11 @@ def main() -> int:
     ap.add_argument("--gemm-variant", default=None, help="big | narrow | tall (kernel tile config)")
     args = ap.parse_args()
 
+    # One hardware queue per stream: the engine's MAIN/SIDE/COMM streams plus torch's and RCCL's own
+    # streams exceed HIP's default of 4, and streams that share a hardware queue also share its
+    # in-order barrier packets (a cross-stream event wait then stalls unrelated work).  Must be set
+    # before the first HIP call of the process.
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     import torch
     import torch.distributed as dist
 

@@ -369,10 +369,14 @@ __global__ __launch_bounds__(CF::NT, CF::WAVES_PER_SIMD) void gemm_kernel(GemmAr
 // ds_read_b64 land on distinct bank halves; the swizzle is applied to the global source address.
 // Requirements (checked by the dispatcher): K-major A, M, N, lda, ldb even, A/B 16-byte aligned.
 namespace glds {
-constexpr int BM = 128, BN = 64, BK = 8, NT = 256;
-constexpr int LDA = BM + 16;                 // A row stride (doubles)
-constexpr int SA = BK * LDA, SB = BK * BN;   // stage sizes (doubles)
-constexpr int STAGE = SA + SB;
+constexpr int BM = 128, BN = 64, NT = 256;
+constexpr int LDA = BM + 16;  // A row stride (doubles)
+template <int BK>
+struct Geo {
+  static constexpr int SA = BK * LDA, SB = BK * BN;  // stage sizes (doubles)
+  static constexpr int STAGE = SA + SB;
+  static constexpr int PIECES = BK / 4 + BK / 8;     // LDS-DMA instructions per wave per slice
+};
 }  // namespace glds
 
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, double* lds_wave_base, int voff) {
@@ -380,20 +384,30 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, double* lds_wave
                                            voff, 0, 0, 0);
 }
 
-// s_waitcnt vmcnt(3 * n) for a runtime n <= 3 (the pieces of n slices may stay in flight)
+// s_waitcnt vmcnt(P * n) for a runtime n <= 3: the pieces of the n most recent slices may stay in
+// flight (P pieces per slice)
+template <int P>
 __device__ __forceinline__ void wait_pieces(int n) {
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+  static_assert(P == 3 || P == 6, "pieces per slice");
+  if (n <= 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else if constexpr (P == 3) {
+    if (n == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if (n == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+  } else {
+    if (n == 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (n == 2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
   }
 }
 
-template <int MODE, int NS, int OCC>
+template <int MODE, int NS, int OCC, int BK>
 __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
   using namespace glds;
   static_assert(NS >= 2 && NS <= 5, "stages");
+  static_assert(BK == 8 || BK == 16, "slice depth");
+  constexpr int SA = Geo<BK>::SA, STAGE = Geo<BK>::STAGE, PIECES = Geo<BK>::PIECES;
   using MF = Mfma<double>;
   using acc_t = MF::acc_t;
   constexpr int ES = 8, TM = 64, TN = 32, MI = 4, NJ = 2, WN = 2;
@@ -477,13 +491,17 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
     double* st = lds + (kt % NS) * STAGE;
     const int k0 = kt * BK;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < BK / 4; ++h) {
       const int kr = wid + 4 * h;
       const bool ok = a_ok && (k0 + kr) < Kd;
       dma16(ra, st + kr * LDA, ok ? ((k0 + kr) * lda + acol) * ES : kOOB);
     }
-    const bool okb = b_ok && (k0 + brow) < Kd;
-    dma16(rb, st + SA + 2 * wid * BN, okb ? ((k0 + brow) * ldb + bcol) * ES : kOOB);
+#pragma unroll
+    for (int h = 0; h < BK / 8; ++h) {  // B rows 2 (wid + 4h) + (lane >> 5)
+      const int br = brow + 8 * h;
+      const bool okb = b_ok && (k0 + br) < Kd;
+      dma16(rb, st + SA + 2 * (wid + 4 * h) * BN, okb ? ((k0 + br) * ldb + bcol) * ES : kOOB);
+    }
   };
   auto compute = [&](int kt) {
     const double* sa = lds + (kt % NS) * STAGE;
@@ -507,14 +525,14 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
   const int nk = (int)((g.K + BK - 1) / BK);
   const int pro = nk < NS - 1 ? nk : NS - 1;  // slices issued ahead
   for (int kt = 0; kt < pro; ++kt) issue(kt);
-  wait_pieces(pro - 1);  // slice 0 landed
+  wait_pieces<PIECES>(pro - 1);  // slice 0 landed
   __builtin_amdgcn_s_barrier();
   for (int kt = 0; kt < nk; ++kt) {
     if (kt + NS - 1 < nk) issue(kt + NS - 1);
     compute(kt);
     // slice kt+1 must have landed (this wave's pieces); the later issued ones may stay in flight
     const int last = (kt + NS - 1 < nk ? kt + NS - 1 : nk - 1);
-    wait_pieces(last - (kt + 1) > 0 ? last - (kt + 1) : 0);
+    wait_pieces<PIECES>(last - (kt + 1) > 0 ? last - (kt + 1) : 0);
     __builtin_amdgcn_s_barrier();
   }
 
@@ -549,11 +567,13 @@ static void launch_glds(const GemmArgs& a0, hipStream_t s) {
   a.group = group;
   const dim3 grid((unsigned)nwg), blk(glds::NT);
   switch (stages) {  // LDS per workgroup: 13.3 KiB per stage
-    case 2: hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 4>), grid, blk, 0, s, a); break;
-    case 6: hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 5>), grid, blk, 0, s, a); break;  // 2 stages, 5 WG/CU
-    case 4: hipLaunchKernelGGL((gemm_glds_f64<MODE, 4, 3>), grid, blk, 0, s, a); break;
-    case 5: hipLaunchKernelGGL((gemm_glds_f64<MODE, 5, 2>), grid, blk, 0, s, a); break;
-    default: hipLaunchKernelGGL((gemm_glds_f64<MODE, 3, 4>), grid, blk, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 4, 8>), grid, blk, 0, s, a); break;
+    case 6: hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 5, 8>), grid, blk, 0, s, a); break;  // 2 stages, 5 WG/CU
+    case 7: hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 3, 16>), grid, blk, 0, s, a); break;  // 16-deep slices
+    case 8: hipLaunchKernelGGL((gemm_glds_f64<MODE, 3, 2, 16>), grid, blk, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((gemm_glds_f64<MODE, 4, 3, 8>), grid, blk, 0, s, a); break;
+    case 5: hipLaunchKernelGGL((gemm_glds_f64<MODE, 5, 2, 8>), grid, blk, 0, s, a); break;
+    default: hipLaunchKernelGGL((gemm_glds_f64<MODE, 3, 4, 8>), grid, blk, 0, s, a); break;
   }
 }
 
