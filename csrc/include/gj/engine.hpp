@@ -91,6 +91,10 @@ class Engine {
   void generate(GenSpec g);
   // host: this rank's real rows, in local order, n columns (ld >= n), fp64.
   void upload_local_rows(const double* host, int64_t ld);
+  // Device-resident I/O: this rank's real rows as a device array of the engine dtype (ld >= n
+  // elements), copied device-to-device (e.g. straight from / into a torch CUDA tensor).
+  void upload_rows_device(const void* src, int64_t ld);
+  void download_rows_device(void* dst, int64_t ld);
   // The input panel as it is right now (dtype elements, ld npad, layout().rows rows).
   void* input_panel() { return X_; }
   double norm_inf();  // collective

@@ -308,6 +308,20 @@ PYBIND11_MODULE(_C, mod) {
              py::gil_scoped_release rel;
              e.eng->upload_local_rows(p, n);
            })
+      .def("upload_rows_device",
+           [](PyEngine& e, uintptr_t ptr, int64_t ld) {
+             if (ld < e.eng->layout().n) throw std::invalid_argument("ld < n");
+             py::gil_scoped_release rel;
+             e.eng->upload_rows_device(reinterpret_cast<const void*>(ptr), ld);
+           },
+           py::arg("ptr"), py::arg("ld"))
+      .def("download_rows_device",
+           [](PyEngine& e, uintptr_t ptr, int64_t ld) {
+             if (ld < e.eng->layout().n) throw std::invalid_argument("ld < n");
+             py::gil_scoped_release rel;
+             e.eng->download_rows_device(reinterpret_cast<void*>(ptr), ld);
+           },
+           py::arg("ptr"), py::arg("ld"))
       .def("input_panel_ptr", [](PyEngine& e) { return (uintptr_t)e.eng->input_panel(); })
       .def("result_panel_ptr", [](PyEngine& e) { return (uintptr_t)e.eng->result_panel(); })
       .def("norm_inf", [](PyEngine& e) {

@@ -259,6 +259,24 @@ void Engine::upload_local_rows(const double* host, int64_t ld) {
   solved_ = false;
 }
 
+void Engine::upload_rows_device(const void* src, int64_t ld) {
+  GenSpec z;
+  z.kind = GenKind::Zero;  // zero + identity on the padded diagonal
+  dev_.generate(opt_.dtype, X_, L_, z, S_MAIN);
+  const int64_t real = real_local_rows();
+  if (real > 0)
+    dev_.copy2d(X_, L_.npad * esz(), src, ld * esz(), L_.n * esz(), real, S_MAIN);
+  dev_.sync_stream(S_MAIN);
+  solved_ = false;
+}
+
+void Engine::download_rows_device(void* dst, int64_t ld) {
+  const int64_t real = real_local_rows();
+  if (real > 0)
+    dev_.copy2d(dst, ld * esz(), out_, L_.npad * esz(), L_.n * esz(), real, S_MAIN);
+  dev_.sync_stream(S_MAIN);
+}
+
 double Engine::norm_inf() {
   dev_.row_abs_max(opt_.dtype, X_, L_.npad, L_, dscratch_, S_MAIN);
   dev_.copy(dhost_, dscratch_, sizeof(double), S_MAIN);

@@ -81,6 +81,8 @@ class GaussJordan:
 
     def inverse(self, A):
         is_torch = isinstance(A, torch.Tensor)
+        if is_torch and A.is_cuda and self.ranks == 1 and self.device in ("auto", "gpu"):
+            return self._inverse_resident(A)
         a = A.detach().to("cpu", torch.float64).numpy() if is_torch else np.asarray(A, dtype=np.float64)
         if a.ndim != 2 or a.shape[0] != a.shape[1]:
             raise ValueError("A must be square")
@@ -95,6 +97,39 @@ class GaussJordan:
         return inv
 
 
+    def _inverse_resident(self, A: torch.Tensor) -> torch.Tensor:
+        """Inverse of a CUDA tensor without host round trips: the rows are copied device-to-device
+        into the engine's panel and the result straight back into a new tensor on A's device."""
+        if A.ndim != 2 or A.shape[0] != A.shape[1]:
+            raise ValueError("A must be square")
+        C = load_native()
+        tdt = torch.float64 if self.dtype == "fp64" else torch.float32
+        a = A.detach().to(tdt).contiguous()
+        n = a.shape[0]
+        idx = a.device.index if a.device.index is not None else torch.cuda.current_device()
+        eng = C.Engine(_hip_device(idx), C.self_comm(), n, int(self.block_size), self.dtype,
+                       int(self.chunk_cols), float(self.eps), bool(self.sync_debug), int(self.depth))
+        torch.cuda.synchronize(a.device)  # A may have been written on torch's stream
+        eng.upload_rows_device(a.data_ptr(), a.stride(0))
+        st = eng.solve()
+        if st["status"] == 1:
+            raise SingularMatrixError("singular matrix")
+        if st["status"] != 0:
+            raise RuntimeError(STATUS.get(st["status"], "error"))
+        out = torch.empty_like(a)
+        eng.download_rows_device(out.data_ptr(), out.stride(0))
+        return out.to(A.dtype)
+
+
+_HIP_DEVICES: dict = {}
+
+
+def _hip_device(idx: int):
+    if idx not in _HIP_DEVICES:
+        _HIP_DEVICES[idx] = load_native().hip_device(idx)
+    return _HIP_DEVICES[idx]
+
+
 def inverse(A, block_size: int = 128, **kw):
     """Inverse of a dense square matrix by block Gauss-Jordan (reference semantics, fixed pivot bug)."""
     return GaussJordan(block_size=block_size, residual="never", **kw).inverse(A)
@@ -106,6 +141,10 @@ def solve(A, b, block_size: int = 128, **kw):
     A single right-hand side runs the native path (x = inv(A) b on the devices, the GEMV next to
     the inverse's rows); a matrix of right-hand sides multiplies by the returned inverse."""
     is_torch = isinstance(A, torch.Tensor)
+    if is_torch and A.is_cuda:  # device-resident: inverse on the GPU, x = inv(A) b next to it
+        inv = inverse(A, block_size=block_size, **kw)
+        bt = b if isinstance(b, torch.Tensor) else torch.as_tensor(np.asarray(b))
+        return inv @ bt.to(device=inv.device, dtype=inv.dtype)
     bn = b.detach().cpu().numpy() if isinstance(b, torch.Tensor) else np.asarray(b, dtype=np.float64)
     if bn.ndim == 1:
         a = A.detach().to("cpu", torch.float64).numpy() if is_torch else np.asarray(A, dtype=np.float64)

@@ -1,6 +1,7 @@
 """End-to-end native engine on the MI355X (HIP kernels + engine + loopback / self comm)."""
 import numpy as np
 import pytest
+import torch
 
 import mpi_jordan_crazy_acceleration_amd as gj
 from mpi_jordan_crazy_acceleration_amd.utils import gauss_jordan_reference, generate_matrix
@@ -112,3 +113,20 @@ def test_block_inverse_variants_in_engine(native, variant):
     inv_ref, _ = gauss_jordan_reference(A, m, 1)
     assert st["offdiag_pivots"] > 0
     assert np.abs(eng.download_local_rows() - inv_ref).max() / np.abs(inv_ref).max() < 1e-9
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_device_resident_inverse_of_cuda_tensor(dtype):
+    """gj.inverse on a CUDA tensor: device-to-device upload/download, result stays on the GPU."""
+    n = 600
+    A = torch.from_numpy(generate_matrix(n, "random", 3)).to(dtype).cuda()
+    inv = gj.inverse(A, block_size=128)
+    assert inv.is_cuda and inv.dtype == dtype and inv.shape == (n, n)
+    ref = np.linalg.inv(A.double().cpu().numpy())
+    rel = np.abs(inv.double().cpu().numpy() - ref).max() / np.abs(ref).max()
+    assert rel < (1e-9 if dtype == torch.float64 else 5e-2), rel
+    b = torch.linspace(-1, 1, n, dtype=dtype, device="cuda")
+    x = gj.solve(A, b, block_size=128)
+    assert x.is_cuda
+    xr = np.linalg.solve(A.double().cpu().numpy(), b.double().cpu().numpy())
+    assert np.abs(x.double().cpu().numpy() - xr).max() / np.abs(xr).max() < (1e-8 if dtype == torch.float64 else 5e-2)

@@ -178,3 +178,19 @@ def test_loopback_detects_collective_mismatch(native):
     assert ok == ["", ""]
     bad = native.loopback_mismatch_probe(1)
     assert all("collective mismatch" in m for m in bad), bad
+
+
+def test_rows_device_io_on_host_executor(native):
+    """upload_rows_device / download_rows_device (the zero-copy path used for CUDA tensors) on the
+    host executor, where the "device" pointers are host arrays."""
+    n, m = 90, 16
+    A = _mat("rand", n, 5)
+    eng = native.Engine(native.host_device(2), native.self_comm(), n, m, "fp64")
+    src = np.zeros((n, n + 3))
+    src[:, :n] = A
+    eng.upload_rows_device(src.ctypes.data, n + 3)
+    assert eng.solve()["status"] == 0
+    out = np.full((n, n + 5), np.nan)
+    eng.download_rows_device(out.ctypes.data, n + 5)
+    assert np.abs(out[:, :n] - np.linalg.inv(A)).max() / np.abs(np.linalg.inv(A)).max() < 1e-10
+    assert np.isnan(out[:, n:]).all()
