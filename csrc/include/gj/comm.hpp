@@ -25,6 +25,12 @@ struct P2POp {
   bool send;
 };
 
+struct BcastOp {
+  void* buf;
+  size_t bytes;
+  int root;
+};
+
 class Comm {
  public:
   virtual ~Comm() = default;
@@ -37,6 +43,11 @@ class Comm {
   virtual void bcast(Device& dev, void* buf, size_t bytes, int root, int s) = 0;
   virtual void allreduce_max(Device& dev, double* buf, size_t count, int s) = 0;
   virtual void group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) = 0;
+  // Several broadcasts (any roots) issued as one group: RCCL runs them concurrently, so pivot rows
+  // owned by different ranks travel over different xGMI links at the same time.
+  virtual void bcast_many(Device& dev, const std::vector<BcastOp>& ops, int s) {
+    for (const auto& o : ops) bcast(dev, o.buf, o.bytes, o.root, s);
+  }
 
   // Host-blocking helpers (once-per-run agreement: errors, timings, residual maxima).
   virtual void barrier(Device& dev) = 0;

@@ -28,6 +28,7 @@ class RcclComm : public Comm {
 
   void allgather(Device& dev, const void* send, void* recv, size_t bytes, int s) override;
   void bcast(Device& dev, void* buf, size_t bytes, int root, int s) override;
+  void bcast_many(Device& dev, const std::vector<BcastOp>& ops, int s) override;
   void allreduce_max(Device& dev, double* buf, size_t count, int s) override;
   void group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) override;
   void barrier(Device& dev) override;

@@ -1,8 +1,9 @@
 // RcclComm: RCCL over xGMI (replaces the reference's MPI layer).
 //
 //   M9  MPI_Allreduce(PivotMin, user op)  -> ncclAllGather of 32-B records (SIDE communicator)
-//   M10 MPI_Bcast(pivot row)              -> ncclBroadcast per column chunk (COMM communicator),
-//                                            pipelined behind the trailing update
+//   M10 MPI_Bcast(pivot row)              -> ncclBroadcast per column chunk and pivot row (COMM
+//                                            communicator), pipelined behind the trailing update;
+//                                            independent ones are issued as one group (bcast_many)
 //   M11 MPI_Send/Recv row swap            -> no per-step traffic; one grouped ncclSend/ncclRecv
 //                                            exchange at the end (finalize)
 //   M14 MPI_Sendrecv_replace ring (residual) -> ncclAllGather of the inverse strips
@@ -75,6 +76,14 @@ void RcclComm::allgather(Device& dev, const void* send, void* recv, size_t bytes
 void RcclComm::bcast(Device& dev, void* buf, size_t bytes, int root, int s) {
   if (n_ == 1) return;
   NCCL_OK(ncclBroadcast(buf, buf, bytes, ncclUint8, root, static_cast<ncclComm_t>(comm_for(s)), st(dev, s)));
+}
+
+void RcclComm::bcast_many(Device& dev, const std::vector<BcastOp>& ops, int s) {
+  if (n_ == 1 || ops.empty()) return;
+  ncclComm_t c = static_cast<ncclComm_t>(comm_for(s));
+  NCCL_OK(ncclGroupStart());
+  for (const auto& o : ops) NCCL_OK(ncclBroadcast(o.buf, o.buf, o.bytes, ncclUint8, o.root, c, st(dev, s)));
+  NCCL_OK(ncclGroupEnd());
 }
 
 void RcclComm::allreduce_max(Device& dev, double* buf, size_t count, int s) {

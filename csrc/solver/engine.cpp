@@ -402,8 +402,9 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
 
 // COMM stream: for every column chunk (in the order MAIN will consume them) and every step of
 // panel v, the owner of s_t forms R_t[chunk] = H_t (X[s_t, chunk] + Lrow_t R_prev[chunk]) outside
-// the panel's columns (those come from the panel piece, later panel blocks zeroed), then all
-// ranks broadcast that stacked row segment.
+// the panel's columns (those come from the panel piece, later panel blocks zeroed), and the row
+// segments are broadcast.  Consecutive segments with the same root go out as one RCCL group; a
+// segment whose owner needs earlier segments of other roots waits for their broadcast first.
 void Engine::chunk_pipeline(int64_t v, bool wait_main) {
   const int par = (int)(v & 1);
   const int64_t m = L_.m, npad = L_.npad;
@@ -426,9 +427,24 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
       ra[0] = c0; rb[0] = c1; nr = 1;
     }
     char* chunk = rb_chunk(par, c);
+    std::vector<BcastOp> bops;
+    auto flush = [&]() {
+      if (bops.empty()) return;
+      const int pb = prof_begin(S_COMM);
+      comm_.bcast_many(dev_, bops, S_COMM);
+      prof_end(PH_BCAST, pb, S_COMM);
+      bops.clear();
+    };
     for (int64_t j = 0; j < q; ++j) {
       const PivotResult& r = piv_[par][j];
       char* seg = chunk + j * m * W * (int64_t)es;
+      // R_j needs the segments of steps < j: the ones its owner did not form itself must have
+      // arrived (the same decision on every rank: it depends only on the pivot owners)
+      for (const auto& o : bops)
+        if (o.root != r.owner) {
+          flush();
+          break;
+        }
       int pe = prof_begin(S_COMM);
       if (r.owner == L_.k) {
         const int64_t sl = r.phys / L_.p;
@@ -454,10 +470,9 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
         }
       }
       prof_end(PH_NORMALISE, pe, S_COMM);
-      pe = prof_begin(S_COMM);
-      comm_.bcast(dev_, seg, (size_t)m * W * es, r.owner, S_COMM);
-      prof_end(PH_BCAST, pe, S_COMM);
+      bops.push_back(BcastOp{seg, (size_t)m * W * es, (int)r.owner});
     }
+    flush();
     dev_.record(ev_b_[par][c], S_COMM);
   }
   dbg_sync();
