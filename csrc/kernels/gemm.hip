@@ -10,19 +10,21 @@
 //   MODE_RESID : per-row partial sums of |A*B - I| (residual, reference matrix_mult_matrix +
 //                                          minus_i + norm, main.cpp:534-667, fused: no D matrix)
 //
-// Tiling (CDNA4, wave64): 128 x 128 output tile per 512-thread workgroup, 8 waves in a 2 x 4 grid,
-// each wave owns 64 x 32 = 4 x 2 MFMA tiles of 16 x 16 (64 accumulator VGPRs for fp64), so two
-// workgroups (4 waves per SIMD) fit in 128 VGPRs and hide each other's C load/store latency.
-// fp64 uses v_mfma_f64_16x16x4_f64 (C/D map col = lane&15, row = (lane>>4) + 4*reg), fp32 uses
-// v_mfma_f32_16x16x4_f32 (row = 4*(lane>>4) + reg).  The accumulator is initialised straight from C
-// in the MFMA C/D layout, so the read-modify-write needs no separate epilogue pass.
-// K is staged through LDS in BK = 16 slices, double-buffered (one barrier per slice); both operands
-// are K-major in LDS with a 16-element pad so the fragment reads (lanes 0-15 / 16-31 on consecutive
-// k rows) are bank-conflict free.  All global traffic uses buffer loads/stores on a per-tile (or
-// per-slice) resource with one shared 32-bit per-lane offset plus SGPR/immediate offsets: that is
-// what keeps the 32 C addresses per lane out of the register file (no spills at 128 VGPRs).
-// f64 MFMA issue is slow (64 cycles per 16x16x4), so LDS bandwidth is a non-issue: 6 ds_read_b64
-// feed 8 MFMAs (512 cycles) per k4 step.
+// Kernels (all wave64, v_mfma_f64_16x16x4_f64 with C/D map col = lane&15, row = (lane>>4) + 4*reg
+// for fp64; v_mfma_f32_16x16x4_f32, row = 4*(lane>>4) + reg, for fp32; the accumulator is loaded
+// straight from C in the C/D layout, so the read-modify-write needs no separate epilogue pass):
+//   * gemm_glds_f64 — the fp64 trailing update (K = depth*m >= 384, enough tiles to fill the chip):
+//     128 x 64 tile per 256-thread workgroup, 2 x 2 waves of 64 x 32, operands staged global -> LDS
+//     by LDS-DMA (buffer_load_dwordx4 ... lds) into a 2-stage ring, counted vmcnt + raw s_barrier,
+//     4 workgroups per CU (82 % MFMA busy at 2.3 GHz: profiles/gemm_variants_k512.md).
+//   * gemm_kernel<T, A-layout, MODE, Cfg> — register-staged tiles for everything else (fp32 deep
+//     updates use the 128 x 128 "squarepf" tile, 110 TF/s; latency-bound panel GEMMs the small
+//     64 x 32 tile; the residual the 128 x 128 tile).  K is staged through LDS in BK-deep slices,
+//     double-buffered, with a 16-element row pad so the fragment reads (lanes 0-15 / 16-31 on
+//     consecutive k rows) are bank-conflict free; Cfg::PF = 2 keeps two slices in registers.
+// All global traffic uses buffer instructions on a per-tile (or per-slice) resource with one 32-bit
+// per-lane offset plus SGPR offsets (no 64-bit address registers, no spills), and masking is done
+// with out-of-range offsets instead of branches (see kOOB).  Tiles are mapped XCD-aware (xcd_remap).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
