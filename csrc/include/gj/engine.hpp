@@ -146,6 +146,9 @@ class Engine {
   int64_t panel_t0(int64_t v) const { return v * d_; }
   int64_t panel_q(int64_t v) const { return std::min<int64_t>(d_, L_.Nr - v * d_); }
   int64_t npanels() const { return (L_.Nr + d_ - 1) / d_; }
+  // trailing-update stream of column chunk c: with two_main_ chunks alternate between MAIN and
+  // MAIN2 so that one chunk's GEMM tail overlaps the next chunk's ramp-up (off by default)
+  int chunk_stream(int64_t c) const { return (two_main_ && (c & 1)) ? S_MAIN2 : S_MAIN; }
   // chunk c of the stacked-rows buffer: (d*m) x W block, ld W
   char* rb_chunk(int par, int64_t c) const {
     return elem(Rb_[par], (int64_t)d_ * L_.m * cb0_[c] * L_.m);
@@ -167,7 +170,10 @@ class Engine {
   // device buffers
   void* X_ = nullptr;       // input / working panel
   void* out_ = nullptr;     // result panel
-  void* At_[2] = {nullptr, nullptr};   // stacked K-major multipliers of a panel, (d*m) x rows
+  // stacked K-major multipliers of a panel, (d*m) x rows, by panel index mod 3: with the trailing
+  // update split over two streams, panel u-2's last chunks may still read theirs while panel u's
+  // look-ahead writes panel u+1's
+  void* At_[3] = {nullptr, nullptr, nullptr};
   void* Rb_[2] = {nullptr, nullptr};   // stacked normalised pivot rows, chunk-major (d*m) x npad
   void* PP_[2] = {nullptr, nullptr};   // panel pieces: R_t restricted to the panel's columns, (d*m) x (d*m)
   void* Lrow_[2][kMaxDepth] = {};      // multipliers of pivot row s_t for earlier panel steps, K-major
@@ -194,7 +200,7 @@ class Engine {
   PivotResult piv_[2][kMaxDepth];      // pivots of the panels in flight (by panel parity)
 
   // events
-  int ev_L_ = -1, ev_main_ = -1, ev_sel_[2] = {-1, -1}, ev_edit_[2] = {-1, -1};
+  int ev_L_ = -1, ev_main_ = -1, ev_main2_ = -1, ev_sel_[2] = {-1, -1}, ev_edit_[2] = {-1, -1};
   int ev_pp_[2][kMaxDepth] = {};
   std::vector<int> ev_c_;        // per chunk: MAIN finished the panel update of that chunk
   std::vector<int> ev_b_[2];     // per chunk: all stacked rows of that chunk broadcast
@@ -203,6 +209,7 @@ class Engine {
   struct PMark { int phase, ev0, ev1; };
   std::vector<PMark> pmarks_;
   bool solved_ = false;
+  bool two_main_ = false;
 };
 
 }  // namespace gj

@@ -71,7 +71,7 @@ class HipDevice : public Device {
   void activate() const;
 
   int dev_ = 0;
-  void* streams_[kNumStreams] = {nullptr, nullptr, nullptr};
+  void* streams_[kNumStreams] = {};
   std::vector<void*> events_;
   void* scratch_[2] = {nullptr, nullptr};
   size_t scratch_sz_[2] = {0, 0};

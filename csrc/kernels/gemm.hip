@@ -3,7 +3,7 @@
 //   MODE_ACC   : C[M x N] += A * B       (the elimination update, reference mult_substr_block
 //                                          main.cpp:151-206 called from the hot loop :1165-1194)
 //                with fused extras: C enters as 0 in columns [zc0, zc1) (the panel's pivot block
-//                columns, X[i,t] := sum -L_i H) and in up to 4 row blocks (the panel's pivot rows,
+//                columns, X[i,t] := sum -L_i H) and in up to 8 row blocks (the panel's pivot rows,
 //                whose multiplier rows the engine turned into [0 .. I .. L] coefficients)
 //   MODE_STORE : C[M x N]  = A * B       (pivot-row normalisation, reference mult_block
 //                                          main.cpp:888-950 called at :1136-1159)

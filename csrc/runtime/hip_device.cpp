@@ -35,7 +35,7 @@ HipDevice::HipDevice(int device_index) : dev_(device_index) {
   HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
   for (int s = 0; s < kNumStreams; ++s) {
     hipStream_t st;
-    const int prio = (s == S_MAIN) ? lo : hi;
+    const int prio = (s == S_MAIN || s == S_MAIN2) ? lo : hi;
     HIP_OK(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, prio));
     streams_[s] = st;
   }
@@ -60,24 +60,26 @@ int HipDevice::reserve_cus(int n, int mode) {
   HIP_OK(hipGetDeviceProperties(&prop, dev_));
   const int ncu = prop.multiProcessorCount;
   n = std::max(0, std::min(n, ncu / 2));
-  HIP_OK(hipStreamSynchronize(hs(streams_[S_MAIN])));
-  HIP_OK(hipStreamDestroy(hs(streams_[S_MAIN])));
-  hipStream_t st;
-  if (n == 0) {
-    int lo = 0, hi = 0;
-    HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    HIP_OK(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, lo));
-  } else {
-    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-    for (int c = 0; c < ncu; ++c) mask[c / 32] |= 1u << (c % 32);
-    const int stride = std::max(1, ncu / n);
-    for (int i = 0; i < n; ++i) {
-      const int c = (mode == 0) ? i : i * stride;
-      mask[c / 32] &= ~(1u << (c % 32));
+  for (int role : {S_MAIN, S_MAIN2}) {
+    HIP_OK(hipStreamSynchronize(hs(streams_[role])));
+    HIP_OK(hipStreamDestroy(hs(streams_[role])));
+    hipStream_t st;
+    if (n == 0) {
+      int lo = 0, hi = 0;
+      HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      HIP_OK(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, lo));
+    } else {
+      std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+      for (int c = 0; c < ncu; ++c) mask[c / 32] |= 1u << (c % 32);
+      const int stride = std::max(1, ncu / n);
+      for (int i = 0; i < n; ++i) {
+        const int c = (mode == 0) ? i : i * stride;
+        mask[c / 32] &= ~(1u << (c % 32));
+      }
+      HIP_OK(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
     }
-    HIP_OK(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+    streams_[role] = st;
   }
-  streams_[S_MAIN] = st;
   reserved_ = n;
   reserve_mode_ = mode;
   return n;

@@ -62,6 +62,11 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
     for (int64_t b = cb0_[c]; b < cb1_[c]; ++b) chunk_of_[b] = (int64_t)c;
 
   alloc_buffers();
+  // Two trailing-update streams (GJ_TWO_MAIN_STREAMS=1): measured slower — N=32768 1283 vs 1167 ms,
+  // p=8 emulation 0.191 vs 0.166 s (two concurrent GEMMs interleave their tiles, lose L2 locality
+  // and crowd out the pivot path) — so off by default.
+  if (const char* e = std::getenv("GJ_TWO_MAIN_STREAMS")) two_main_ = std::atoi(e) != 0;
+  two_main_ = two_main_ && cb0_.size() > 1;
 
   // CU reservation for the latency-bound panel factorisation (GJ_RESERVE_CUS overrides).
   int rc = opt_.reserve_cus;
@@ -85,7 +90,7 @@ void Engine::alloc_buffers() {
   const size_t panel = (size_t)rows * npad * es;
   int64_t wmax = 0;
   for (size_t c = 0; c < cb0_.size(); ++c) wmax = std::max(wmax, chunk_w((int64_t)c));
-  const size_t need = 2 * panel + 2 * (size_t)dm * rows * es + 2 * (size_t)dm * npad * es +
+  const size_t need = 2 * panel + 3 * (size_t)dm * rows * es + 2 * (size_t)dm * npad * es +
                       (size_t)std::max<int64_t>(L_.nblk, 1) * m * m * es + (size_t)m * wmax * es;
   if (dev_.on_gpu()) {
     size_t avail = dev_.free_memory();
@@ -95,8 +100,8 @@ void Engine::alloc_buffers() {
   }
   X_ = dev_.alloc(panel);
   out_ = dev_.alloc(panel);
+  for (int i = 0; i < 3; ++i) At_[i] = dev_.alloc((size_t)dm * rows * es);
   for (int i = 0; i < 2; ++i) {
-    At_[i] = dev_.alloc((size_t)dm * rows * es);
     Rb_[i] = dev_.alloc((size_t)dm * npad * es);
     PP_[i] = dev_.alloc((size_t)dm * dm * es);
     for (int j = 0; j < d_; ++j) {
@@ -125,6 +130,7 @@ void Engine::alloc_buffers() {
 
   ev_L_ = dev_.create_event();
   ev_main_ = dev_.create_event();
+  ev_main2_ = dev_.create_event();
   for (int i = 0; i < 2; ++i) {
     ev_sel_[i] = dev_.create_event();
     ev_edit_[i] = dev_.create_event();
@@ -137,8 +143,8 @@ void Engine::alloc_buffers() {
 void Engine::free_buffers() {
   std::vector<void*> dptrs = {X_, out_, T_, RP_, inv_, scores_, valid_, pos_, phys_at_, used_, seq_,
                               myrec_, recs_, piv_dev_, dscratch_, iscratch_};
+  for (int i = 0; i < 3; ++i) dptrs.push_back(At_[i]);
   for (int i = 0; i < 2; ++i) {
-    dptrs.push_back(At_[i]);
     dptrs.push_back(Rb_[i]);
     dptrs.push_back(PP_[i]);
     for (int j = 0; j < kMaxDepth; ++j) {
@@ -322,7 +328,7 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
   const size_t es = esz();
   for (int64_t j = 0; j < q; ++j) {
     const int64_t t = t0 + j;
-    void* Lt = elem(At_[par], j * m * rows);
+    void* Lt = elem(At_[v % 3], j * m * rows);
     if (j == 0) {
       dev_.wait(S_SIDE, ev_L_);
     } else {
@@ -332,7 +338,7 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
       if (rows > 0) {
         GemmExtra ex = pivot_rows_extra(par, j);
         ex.latency = true;
-        dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, m, j * m, At_[par], rows,
+        dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, m, j * m, At_[v % 3], rows,
                   elem(PP_[par], j * m), dm, elem(X_, t * m), npad, S_SIDE, ex);
         dev_.extract_neg_t(opt_.dtype, Lt, rows, X_, npad, rows, t * m, m, S_SIDE);
       }
@@ -355,11 +361,11 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
     if (owner) {
       st.bcast_bytes += double(m) * npad * es;
       if (j > 0)  // multipliers of row s_t for steps t0..t-1 (K-major j*m x m)
-        dev_.copy2d(Lrow_[par][j], m * es, elem(At_[par], sl * m), rows * es, m * es, j * m, S_SIDE);
+        dev_.copy2d(Lrow_[par][j], m * es, elem(At_[v % 3], sl * m), rows * es, m * es, j * m, S_SIDE);
       dev_.copy(Ht_[par][j], elem(inv_, sl * m * m), (size_t)m * m * es, S_SIDE);
       // multiplier rows of s_t: earlier segments -> 0, own segment -> I
-      dev_.memset2d(elem(At_[par], sl * m), rows * es, m * es, (j + 1) * m, S_SIDE);
-      dev_.add_diag(opt_.dtype, elem(At_[par], j * m * rows + sl * m), rows, m, 1.0, S_SIDE);
+      dev_.memset2d(elem(At_[v % 3], sl * m), rows * es, m * es, (j + 1) * m, S_SIDE);
+      dev_.add_diag(opt_.dtype, elem(At_[v % 3], j * m * rows + sl * m), rows, m, 1.0, S_SIDE);
     }
     prof_end(PH_EDITS, pe, S_SIDE);
     dev_.record(ev_edit_[par], S_SIDE);
@@ -478,31 +484,39 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
   dbg_sync();
 }
 
-// MAIN stream: the depth-q trailing update of panel u.  The next panel's block columns are done
-// first (look-ahead) so its pivot search can start; then every other chunk.
+// MAIN streams: the depth-q trailing update of panel u.  The next panel's block columns are done
+// first (look-ahead) so its pivot search can start; then every other chunk.  Chunk c always runs on
+// chunk_stream(c), so chunk c of panel u+1 is ordered after chunk c of panel u by its stream alone,
+// and the two streams overlap one chunk's GEMM tail with the next chunk's ramp-up.  Hazards across
+// the streams: the multiplier panels are triple-buffered (At_[u % 3]); Rb_[par] chunk c is rewritten
+// by the COMM stream only after ev_c_[c] of the following panel (same stream as its readers).
 void Engine::big_update(int64_t u) {
-  const int par = (int)(u & 1), npar = par ^ 1;
+  const int par = (int)(u & 1);
+  void* At = At_[u % 3];
+  void* At_next = At_[(u + 1) % 3];
   const int64_t m = L_.m, rows = L_.rows, npad = L_.npad;
   const int64_t t0 = panel_t0(u), q = panel_q(u), K = q * m;
   const int64_t C = (int64_t)cb0_.size();
   const bool has_next = (u + 1 < npanels());
   const GemmExtra prows = pivot_rows_extra(par, q);
   dev_.wait(S_MAIN, ev_edit_[par]);
+  if (two_main_) dev_.wait(S_MAIN2, ev_edit_[par]);
   int64_t x0 = -1, x1 = -1;  // look-ahead columns
   if (has_next) {
     const int64_t tn = panel_t0(u + 1), qn = panel_q(u + 1), cn = chunk_of_[tn];
+    const int ms = chunk_stream(cn);
     x0 = tn * m;
     x1 = (tn + qn) * m;
-    dev_.wait(S_MAIN, ev_b_[par][cn]);
-    const int pe = prof_begin(S_MAIN);
+    dev_.wait(ms, ev_b_[par][cn]);
+    const int pe = prof_begin(ms);
     if (rows > 0) {
-      dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, x1 - x0, K, At_[par], rows,
+      dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, x1 - x0, K, At, rows,
                 rb_chunk(par, cn) + (x0 - cb0_[cn] * m) * (int64_t)esz(), chunk_w(cn), elem(X_, x0),
-                npad, S_MAIN, prows);
-      dev_.extract_neg_t(opt_.dtype, At_[npar], rows, X_, npad, rows, x0, m, S_MAIN);
+                npad, ms, prows);
+      dev_.extract_neg_t(opt_.dtype, At_next, rows, X_, npad, rows, x0, m, ms);
     }
-    prof_end(PH_UPDATE, pe, S_MAIN);
-    dev_.record(ev_L_, S_MAIN);
+    prof_end(PH_UPDATE, pe, ms);
+    dev_.record(ev_L_, ms);
     dbg_sync();
   }
   const int64_t start = has_next ? chunk_of_[panel_t0(u + 1)] : 0;
@@ -510,8 +524,9 @@ void Engine::big_update(int64_t u) {
   for (int64_t i = 0; i < C; ++i) {
     const int64_t c = (start + i) % C;
     const int64_t c0 = cb0_[c] * m, c1 = cb1_[c] * m, W = c1 - c0;
-    dev_.wait(S_MAIN, ev_b_[par][c]);
-    const int pe = prof_begin(S_MAIN);
+    const int ms = chunk_stream(c);
+    dev_.wait(ms, ev_b_[par][c]);
+    const int pe = prof_begin(ms);
     int64_t ra[2], rb[2], nr = 0;
     if (has_next && x0 >= c0 && x0 < c1) {
       if (x0 > c0) { ra[nr] = c0; rb[nr] = x0; ++nr; }
@@ -524,12 +539,11 @@ void Engine::big_update(int64_t u) {
         GemmExtra ex = prows;
         ex.zc0 = pc0 - ra[z];  // the panel's own block columns enter as 0
         ex.zc1 = pc1 - ra[z];
-        dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, rb[z] - ra[z], K, At_[par], rows,
-                  rb_chunk(par, c) + (ra[z] - c0) * (int64_t)esz(), W, elem(X_, ra[z]), npad, S_MAIN,
-                  ex);
+        dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, rb[z] - ra[z], K, At, rows,
+                  rb_chunk(par, c) + (ra[z] - c0) * (int64_t)esz(), W, elem(X_, ra[z]), npad, ms, ex);
       }
-    prof_end(PH_UPDATE, pe, S_MAIN);
-    dev_.record(ev_c_[c], S_MAIN);
+    prof_end(PH_UPDATE, pe, ms);
+    dev_.record(ev_c_[c], ms);
   }
   dbg_sync();
 }
@@ -583,6 +597,10 @@ SolveStats Engine::solve() {
     return st;
   }
 
+  if (two_main_) {  // the last chunks may still run on MAIN2
+    dev_.record(ev_main2_, S_MAIN2);
+    dev_.wait(S_MAIN, ev_main2_);
+  }
   {
     const int pe = prof_begin(S_COMM);
     finalize(st.pivots);
