@@ -56,6 +56,8 @@ class Device {
   virtual void* alloc(size_t bytes) = 0;
   virtual void release(void* p) = 0;
   virtual void* alloc_pinned(size_t bytes) = 0;
+  // Fine-grained (coherent) pinned host memory: kernels store into it and the host polls it.
+  virtual void* alloc_pinned_coherent(size_t bytes) { return alloc_pinned(bytes); }
   virtual void release_pinned(void* p) = 0;
   virtual size_t free_memory() const = 0;
   virtual void memset0(void* p, size_t bytes, int s) = 0;
@@ -100,10 +102,19 @@ class Device {
   // Local argmin over this rank's candidates -> *out.
   virtual void pivot_local(const double* scores, const int32_t* valid, const int32_t* used,
                            const int32_t* pos, const Layout& L, PivotRec* out, int s) = 0;
-  // Global selection over p records + book-keeping (pivot_commit) -> *out.
+  // Global selection over p records + book-keeping (pivot_commit) -> *out, and the same record to
+  // host_out (pinned host memory the host polls: its `step` field is written last, after a
+  // system-scope fence) when host_out != nullptr.
   virtual void pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos,
                             int32_t* phys_at, int32_t* used, int32_t* seq, PivotResult* out,
-                            int s) = 0;
+                            PivotResult* host_out, int s) = 0;
+  // Owner-side edits of a pivot step, fused (one launch): for the pivot's local block row b0 (rows
+  // row0 .. row0+m-1 of the K-major multiplier panel At, ld ldl) save the multipliers of the panel's
+  // earlier steps, lrow[k*m + c] = At[k*ldl + row0 + c] for k < j*m, then set those rows of At to
+  // [0 .. 0 | I] over the first (j+1)*m K-rows (identity in segment j), and copy the m x m block
+  // inverse: ht[e] = inv_blk[e], e < m*m.
+  virtual void owner_edits(DType dt, void* At, int64_t ldl, int64_t row0, int64_t j, int64_t m,
+                           void* lrow, void* ht, const void* inv_blk, int s) = 0;
   // R[i*ldr + j] = H[i][j] = Ht[j*m + i]   (the pivot column block of the broadcast row).
   virtual void h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, int s) = 0;
   virtual void gemm(DType dt, GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const void* A,

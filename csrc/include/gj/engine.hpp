@@ -134,8 +134,9 @@ class Engine {
   void finalize(const std::vector<int32_t>& seq);
   double residual_common();
   void dbg_sync();
-  // Host wait for a pivot result with failure detection (Comm::check_health + timeout).
-  void wait_pivot(int ev, int64_t step, double& host_wait);
+  // Host wait for the pivot result of `step` (pinned slot par) with failure detection
+  // (Comm::check_health + timeout).
+  void wait_pivot(int par, int64_t step, double& host_wait);
   // profiling: begin() records a timing event on stream s, end() closes the interval
   int prof_begin(int s);
   void prof_end(int phase, int ev0, int s);

@@ -190,7 +190,8 @@ void pivot_local(const double* scores, const int32_t* valid, const int32_t* used
 }
 
 __global__ void pivot_global_kernel(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos,
-                                    int32_t* phys_at, int32_t* used, int32_t* seq, PivotResult* out) {
+                                    int32_t* phys_at, int32_t* used, int32_t* seq, PivotResult* out,
+                                    PivotResult* host_out) {
   if (threadIdx.x != 0) return;
   PivotRec best = pivot_invalid();
   for (int32_t q = 0; q < p; ++q)
@@ -213,12 +214,55 @@ __global__ void pivot_global_kernel(const PivotRec* recs, int32_t p, int32_t t, 
     r.score = 0.0;
   }
   *out = r;
+  if (host_out) {  // the host polls `step`: every other field first, then a system-scope fence
+    volatile PivotResult* h = host_out;
+    h->found = r.found;
+    h->phys = r.phys;
+    h->owner = r.owner;
+    h->logical = r.logical;
+    h->score = r.score;
+    __threadfence_system();
+    h->step = r.step;
+    __threadfence_system();
+  }
 }
 
 void pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos, int32_t* phys_at,
-                  int32_t* used, int32_t* seq, PivotResult* out, hipStream_t s) {
+                  int32_t* used, int32_t* seq, PivotResult* out, PivotResult* host_out, hipStream_t s) {
   hipLaunchKernelGGL(pivot_global_kernel, dim3(1), dim3(64), 0, s, recs, p, t, pos, phys_at, used, seq,
-                     out);
+                     out, host_out);
+}
+
+// ---------------------------------------------------------------- owner edits (one launch)
+template <typename T>
+__global__ __launch_bounds__(256) void owner_edits_kernel(T* At, int64_t ldl, int64_t row0, int64_t j,
+                                                          int64_t m, T* lrow, T* ht, const T* inv_blk) {
+  const int64_t nrow = (j + 1) * m, total = nrow * m;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total + m * m;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    if (e < total) {
+      const int64_t k = e / m, c = e - k * m;
+      T* x = At + k * ldl + row0 + c;
+      if (k < j * m) lrow[k * m + c] = *x;
+      *x = (k - j * m == c) ? T(1) : T(0);
+    } else {
+      ht[e - total] = inv_blk[e - total];
+    }
+  }
+}
+
+void owner_edits(DType dt, void* At, int64_t ldl, int64_t row0, int64_t j, int64_t m, void* lrow,
+                 void* ht, const void* inv_blk, hipStream_t s) {
+  const int64_t work = (j + 2) * m * m;
+  const unsigned grid = grid_for(work, 256, 256);
+  if (dt == DType::F64)
+    hipLaunchKernelGGL(owner_edits_kernel<double>, dim3(grid), dim3(256), 0, s, static_cast<double*>(At),
+                       ldl, row0, j, m, static_cast<double*>(lrow), static_cast<double*>(ht),
+                       static_cast<const double*>(inv_blk));
+  else
+    hipLaunchKernelGGL(owner_edits_kernel<float>, dim3(grid), dim3(256), 0, s, static_cast<float*>(At),
+                       ldl, row0, j, m, static_cast<float*>(lrow), static_cast<float*>(ht),
+                       static_cast<const float*>(inv_blk));
 }
 
 // ---------------------------------------------------------------- permute_blocks

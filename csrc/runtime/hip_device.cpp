@@ -108,6 +108,11 @@ void* HipDevice::alloc_pinned(size_t bytes) {
   HIP_OK(hipHostMalloc(&p, bytes ? bytes : 64, hipHostMallocDefault));
   return p;
 }
+void* HipDevice::alloc_pinned_coherent(size_t bytes) {
+  void* p = nullptr;
+  HIP_OK(hipHostMalloc(&p, bytes ? bytes : 64, hipHostMallocCoherent));
+  return p;
+}
 void HipDevice::release_pinned(void* p) { (void)hipHostFree(p); }
 size_t HipDevice::free_memory() const {
   activate();
@@ -216,8 +221,13 @@ void HipDevice::pivot_local(const double* scores, const int32_t* valid, const in
 }
 void HipDevice::pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos,
                              int32_t* phys_at, int32_t* used, int32_t* seq, PivotResult* out,
-                             int s) {
-  kern::pivot_global(recs, p, t, pos, phys_at, used, seq, out, hs(streams_[s]));
+                             PivotResult* host_out, int s) {
+  kern::pivot_global(recs, p, t, pos, phys_at, used, seq, out, host_out, hs(streams_[s]));
+  check_launch();
+}
+void HipDevice::owner_edits(DType dt, void* At, int64_t ldl, int64_t row0, int64_t j, int64_t m,
+                            void* lrow, void* ht, const void* inv_blk, int s) {
+  kern::owner_edits(dt, At, ldl, row0, j, m, lrow, ht, inv_blk, hs(streams_[s]));
   check_launch();
 }
 void HipDevice::h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, int s) {

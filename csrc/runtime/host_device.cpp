@@ -7,6 +7,7 @@
 #include "gj/host_device.hpp"
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -251,7 +252,8 @@ void HostDevice::pivot_local(const double* scores, const int32_t* valid, const i
 }
 
 void HostDevice::pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos,
-                              int32_t* phys_at, int32_t* used, int32_t* seq, PivotResult* out, int) {
+                              int32_t* phys_at, int32_t* used, int32_t* seq, PivotResult* out,
+                              PivotResult* host_out, int) {
   PivotRec best = pivot_invalid();
   for (int32_t q = 0; q < p; ++q)
     if (pivot_better(recs[q], best, p)) best = recs[q];
@@ -271,6 +273,27 @@ void HostDevice::pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_
     r.logical = -1;
   }
   *out = r;
+  if (host_out) *host_out = r;
+}
+
+void HostDevice::owner_edits(DType dt, void* At, int64_t ldl, int64_t row0, int64_t j, int64_t m,
+                             void* lrow, void* ht, const void* inv_blk, int) {
+  auto run = [&](auto* a, auto* lr, auto* h, const auto* inv) {
+    using T = std::remove_pointer_t<decltype(a)>;
+    for (int64_t k = 0; k < (j + 1) * m; ++k)
+      for (int64_t c = 0; c < m; ++c) {
+        T& x = a[k * ldl + row0 + c];
+        if (k < j * m) lr[k * m + c] = x;
+        x = (k - j * m == c) ? T(1) : T(0);
+      }
+    for (int64_t e = 0; e < m * m; ++e) h[e] = inv[e];
+  };
+  if (dt == DType::F64)
+    run(static_cast<double*>(At), static_cast<double*>(lrow), static_cast<double*>(ht),
+        static_cast<const double*>(inv_blk));
+  else
+    run(static_cast<float*>(At), static_cast<float*>(lrow), static_cast<float*>(ht),
+        static_cast<const float*>(inv_blk));
 }
 
 void HostDevice::h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, int) {

@@ -24,6 +24,7 @@
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -124,7 +125,7 @@ void Engine::alloc_buffers() {
   dscratch_ = static_cast<double*>(dev_.alloc(sizeof(double) * 64));
   ihost_len_ = std::max<int64_t>(L_.Nr, 16) * 2 + 16;
   iscratch_ = static_cast<int32_t*>(dev_.alloc(sizeof(int32_t) * ihost_len_));
-  piv_host_ = static_cast<PivotResult*>(dev_.alloc_pinned(sizeof(PivotResult) * 2));
+  piv_host_ = static_cast<PivotResult*>(dev_.alloc_pinned_coherent(sizeof(PivotResult) * 2));
   ihost_ = static_cast<int32_t*>(dev_.alloc_pinned(sizeof(int32_t) * ihost_len_));
   dhost_ = static_cast<double*>(dev_.alloc_pinned(sizeof(double) * 64));
 
@@ -170,14 +171,16 @@ const char* phase_name(int ph) {
   return (ph >= 0 && ph < kNumPhases) ? names[ph] : "?";
 }
 
-// Spin on the event (the wait is on the critical path of small problems), checking the
-// communicator every 20 ms and giving up after comm_timeout_s: a dead peer turns into an error on
-// every surviving rank instead of a hang (reference: none).
-void Engine::wait_pivot(int ev, int64_t step, double& host_wait) {
+// Spin on the pinned pivot record (the wait is on the critical path of small problems: polling host
+// memory reacts in ~1 us where an event query took ~25), checking the communicator every 20 ms and
+// giving up after comm_timeout_s: a dead peer turns into an error on every surviving rank instead
+// of a hang (reference: none).
+void Engine::wait_pivot(int par, int64_t step, double& host_wait) {
   const double w0 = now_s();
   double next_check = w0 + 0.02;
   int spins = 0;
-  while (!dev_.query_event(ev)) {
+  const volatile int32_t* st = &piv_host_[par].step;
+  while (*st != (int32_t)step) {
     if (++spins > 2000) std::this_thread::yield();
     const double t = now_s();
     if (t >= next_check) {
@@ -191,6 +194,7 @@ void Engine::wait_pivot(int ev, int64_t step, double& host_wait) {
       next_check = t + 0.02;
     }
   }
+  std::atomic_thread_fence(std::memory_order_acquire);
   host_wait += now_s() - w0;
 }
 
@@ -302,8 +306,10 @@ void Engine::select(int64_t t, const void* Lt) {
   prof_end(PH_PIVOT, pe, S_SIDE);
   pe = prof_begin(S_SIDE);
   comm_.allgather(dev_, myrec_, recs_, sizeof(PivotRec), S_SIDE);
-  dev_.pivot_global(recs_, (int32_t)L_.p, (int32_t)t, pos_, phys_at_, used_, seq_, piv_dev_, S_SIDE);
-  dev_.copy(&piv_host_[par], piv_dev_, sizeof(PivotResult), S_SIDE);
+  // the result goes straight to pinned host memory (no copy kernel); the host polls its step field
+  piv_host_[par].step = -1;
+  dev_.pivot_global(recs_, (int32_t)L_.p, (int32_t)t, pos_, phys_at_, used_, seq_, piv_dev_,
+                    &piv_host_[par], S_SIDE);
   prof_end(PH_EXCHANGE, pe, S_SIDE);
   dev_.record(ev_sel_[par], S_SIDE);
   dbg_sync();
@@ -345,7 +351,7 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
       prof_end(PH_COLUMN, pe, S_SIDE);
     }
     select(t, Lt);
-    wait_pivot(ev_sel_[t & 1], t, host_wait);
+    wait_pivot((int)(t & 1), t, host_wait);
     const PivotResult r = piv_host_[t & 1];
     if (!r.found) {
       dev_.sync_all();
@@ -360,12 +366,10 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
     int pe = prof_begin(S_SIDE);
     if (owner) {
       st.bcast_bytes += double(m) * npad * es;
-      if (j > 0)  // multipliers of row s_t for steps t0..t-1 (K-major j*m x m)
-        dev_.copy2d(Lrow_[par][j], m * es, elem(At_[v % 3], sl * m), rows * es, m * es, j * m, S_SIDE);
-      dev_.copy(Ht_[par][j], elem(inv_, sl * m * m), (size_t)m * m * es, S_SIDE);
-      // multiplier rows of s_t: earlier segments -> 0, own segment -> I
-      dev_.memset2d(elem(At_[v % 3], sl * m), rows * es, m * es, (j + 1) * m, S_SIDE);
-      dev_.add_diag(opt_.dtype, elem(At_[v % 3], j * m * rows + sl * m), rows, m, 1.0, S_SIDE);
+      // one launch: multipliers of row s_t for steps t0..t-1 -> Lrow (K-major j*m x m), H_t^T -> Ht,
+      // and the multiplier rows of s_t become [0 .. 0 | I] (earlier segments 0, own segment I)
+      dev_.owner_edits(opt_.dtype, At_[v % 3], rows, sl * m, j, m, Lrow_[par][j], Ht_[par][j],
+                       elem(inv_, sl * m * m), S_SIDE);
     }
     prof_end(PH_EDITS, pe, S_SIDE);
     dev_.record(ev_edit_[par], S_SIDE);
