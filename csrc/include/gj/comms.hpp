@@ -12,8 +12,9 @@
 namespace gj {
 
 // ---------------------------------------------------------------- RCCL over xGMI
-// One RCCL communicator per stream role that issues collectives (SIDE: pivot records and
-// once-per-run maxima; COMM: pivot-row broadcast, finalisation exchange, residual all-gather),
+// One RCCL communicator per stream role that issues collectives (SIDE: pivot records, panel-piece
+// broadcasts and once-per-run maxima; COMM: pivot-row chunk broadcasts, finalisation exchange,
+// residual all-gather),
 // so collectives of different roles can never be reordered against each other across ranks.
 class RcclComm : public Comm {
  public:

@@ -53,7 +53,7 @@ enum Phase : int {
   PH_PIVOT,        // SIDE: batched candidate inverses + local argmin
   PH_EXCHANGE,     // SIDE: pivot record all-gather + global argmin + 32-B readback
   PH_EDITS,        // SIDE: owner-side multiplier / H edits
-  PH_PIECES,       // COMM: panel pieces (owner GEMMs) + their broadcast
+  PH_PIECES,       // SIDE: panel piece (fused owner kernel) + its broadcast
   PH_NORMALISE,    // COMM: owner normalises its pivot rows chunk by chunk (GEMM)
   PH_BCAST,        // COMM: pivot-row chunk broadcasts
   PH_UPDATE,       // MAIN: depth-d trailing update (the MFMA GEMM)

@@ -375,9 +375,11 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
     dev_.record(ev_edit_[par], S_SIDE);
     dbg_sync();
 
-    // panel piece PP_t (m x q*m, ld dm) on COMM
-    dev_.wait(S_COMM, ev_edit_[par]);
-    pe = prof_begin(S_COMM);
+    // panel piece PP_t (m x q*m, ld dm), right behind the edits on SIDE: the next step's column
+    // update needs it, so the whole per-step chain stays on one stream (no cross-stream hops).
+    // (A fused one-launch piece kernel was measured slower: its register/LDS footprint exceeds
+    // what a retiring trailing-update workgroup frees, so it waited for CUs; small GEMMs fit.)
+    pe = prof_begin(S_SIDE);
     void* pp = elem(PP_[par], j * m * dm);
     GemmExtra lat;
     lat.latency = true;
@@ -388,22 +390,22 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
         if (jc < j) {  // earlier pivot column: sum over steps jc..j-1 only, no input
           dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, m, (j - jc) * m,
                     elem(Lrow_[par][j], jc * m * m), m, elem(PP_[par], jc * m * dm + jc * m), dm, rp,
-                    dm, S_COMM, lat);
+                    dm, S_SIDE, lat);
         } else {  // later panel column: look-ahead value + all earlier steps
           dev_.copy2d(rp, dm * es, elem(X_, sl * m * npad + (t0 + jc) * m), npad * es, m * es, m,
-                      S_COMM);
+                      S_SIDE);
           if (j > 0)
             dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, m, m, j * m, Lrow_[par][j], m,
-                      elem(PP_[par], jc * m), dm, rp, dm, S_COMM, lat);
+                      elem(PP_[par], jc * m), dm, rp, dm, S_SIDE, lat);
         }
       }
       dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, q * m, m, Ht_[par][j], m, RP_, dm, pp,
-                dm, S_COMM, lat);
-      dev_.h_block(opt_.dtype, elem(pp, j * m), dm, Ht_[par][j], m, S_COMM);
+                dm, S_SIDE, lat);
+      dev_.h_block(opt_.dtype, elem(pp, j * m), dm, Ht_[par][j], m, S_SIDE);
     }
-    comm_.bcast(dev_, pp, (size_t)m * dm * es, r.owner, S_COMM);
-    prof_end(PH_PIECES, pe, S_COMM);
-    dev_.record(ev_pp_[par][j], S_COMM);
+    comm_.bcast(dev_, pp, (size_t)m * dm * es, r.owner, S_SIDE);
+    prof_end(PH_PIECES, pe, S_SIDE);
+    dev_.record(ev_pp_[par][j], S_SIDE);
     dbg_sync();
   }
   chunk_pipeline(v, wait_main);
@@ -424,6 +426,7 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
   const bool has_next = (v + 1 < npanels());
   const int64_t start = has_next ? chunk_of_[panel_t0(v + 1)] : 0;
   const int64_t pc0 = t0 * m, pc1 = (t0 + q) * m;  // panel columns
+  dev_.wait(S_COMM, ev_pp_[par][q - 1]);  // all panel pieces, multiplier rows and H_t (SIDE)
   for (int64_t i = 0; i < C; ++i) {
     const int64_t c = (start + i) % C;
     const int64_t c0 = cb0_[c] * m, c1 = cb1_[c] * m, W = c1 - c0;

@@ -113,7 +113,7 @@ def test_axb_plumbing_512(gj_bin, tmp_path):
     assert rc == 0, err
     assert "Ax-b residual:" in out
     res = float(out.strip().split("\n")[-1].split()[-1])
-    assert res < 1e-10
+    assert res < 1e-9  # block Gauss-Jordan on a random 512 matrix: ~1e-10 (summation-order dependent)
     x = np.loadtxt(xf)
     A = generate_matrix(512, "random", 5)
     assert np.abs(A @ x).max() > 0
