@@ -561,10 +561,11 @@ static void launch_glds(const GemmArgs& a0, hipStream_t s) {
   if (nwg <= 0) return;
   // Pipeline depth / occupancy, measured at 32768 x 4096 x 512 alone: 2 stages at 5 WG/CU ("6")
   // 62.6 TF/s, at 4 WG/CU 61.2; 3/4/5 stages at 4/3/2 WG/CU 59.4/59.1/53.7.  Inside the solver the
-  // 4-WG/CU form wins (N=32768: 1155 vs 1205 ms, profiles/cu_reserve_sweep.md): the register/LDS
-  // room it leaves lets the latency-bound pivot-path kernels start without waiting for the GEMM
-  // to drain.  Tile rows are walked in groups of 4 (+0.5-1 %).
-  static const int stages = getenv("GJ_GLDS_STAGES") ? atoi(getenv("GJ_GLDS_STAGES")) : 2;
+  // 4-WG/CU form beats 5 (N=32768: 1155 vs 1205 ms, profiles/cu_reserve_sweep.md) and 3 WG/CU
+  // ("9") beats 4 again (1138 vs 1147 ms, 60.5 vs 60.4 TF/s alone; profiles/gemm_variants_k512.md):
+  // the register/LDS room it leaves lets the latency-bound pivot-path and RCCL kernels start
+  // without waiting for the GEMM to drain.  Tile rows are walked in groups of 4 (+0.5-1 %).
+  static const int stages = getenv("GJ_GLDS_STAGES") ? atoi(getenv("GJ_GLDS_STAGES")) : 9;
   static const int group = getenv("GJ_GEMM_GROUP") ? atoi(getenv("GJ_GEMM_GROUP")) : 4;
   a.group = group;
   const dim3 grid((unsigned)nwg), blk(glds::NT);
@@ -572,6 +573,7 @@ static void launch_glds(const GemmArgs& a0, hipStream_t s) {
     case 2: hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 4, 8>), grid, blk, 0, s, a); break;
     case 6: hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 5, 8>), grid, blk, 0, s, a); break;  // 2 stages, 5 WG/CU
     case 7: hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 3, 16>), grid, blk, 0, s, a); break;  // 16-deep slices
+    case 9: hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 3, 8>), grid, blk, 0, s, a); break;   // 3 WG/CU
     case 8: hipLaunchKernelGGL((gemm_glds_f64<MODE, 3, 2, 16>), grid, blk, 0, s, a); break;
     case 4: hipLaunchKernelGGL((gemm_glds_f64<MODE, 4, 3, 8>), grid, blk, 0, s, a); break;
     case 5: hipLaunchKernelGGL((gemm_glds_f64<MODE, 5, 2, 8>), grid, blk, 0, s, a); break;
