@@ -559,12 +559,15 @@ static void launch_glds(const GemmArgs& a0, hipStream_t s) {
   a.tiles_n = (int)((a.N + glds::BN - 1) / glds::BN);
   const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;
   if (nwg <= 0) return;
-  // Pipeline depth / occupancy, measured at 32768 x 4096 x 512 alone: 2 stages at 5 WG/CU ("6")
-  // 62.6 TF/s, at 4 WG/CU 61.2; 3/4/5 stages at 4/3/2 WG/CU 59.4/59.1/53.7.  Inside the solver the
-  // 4-WG/CU form beats 5 (N=32768: 1155 vs 1205 ms, profiles/cu_reserve_sweep.md) and 3 WG/CU
-  // ("9") beats 4 again (1138 vs 1147 ms, 60.5 vs 60.4 TF/s alone; profiles/gemm_variants_k512.md):
-  // the register/LDS room it leaves lets the latency-bound pivot-path and RCCL kernels start
-  // without waiting for the GEMM to drain.  Tile rows are walked in groups of 4 (+0.5-1 %).
+  // Template args <stages, W, slice>: W is __launch_bounds__' minimum waves per SIMD (a VGPR cap for
+  // the compiler).  Residency = min(VGPR, LDS limits), from -Rpass-analysis=kernel-resource-usage:
+  // <2,5,8> 96 VGPRs -> 5 workgroups/CU; <2,4,8> 111 and <2,3,8> 112 -> 4 (LDS would allow 6);
+  // 3/4/5 stages -> 4/3/2.  Measured at 32768 x 4096 x 512 alone: <2,5,8> ("6") 62.6 TF/s, <2,4,8>
+  // ("2") 61.2, <2,3,8> ("9") 60.5; 3/4/5 stages 59.4/59.1/53.7.  Inside the solver the order
+  // flips: N=32768 <2,3,8> 1138 ms, <2,4,8> 1147, <2,5,8> 1205 (profiles/cu_reserve_sweep.md,
+  // profiles/gemm_variants_k512.md): at 4 workgroups per CU the pivot-path kernels find room, and
+  // the <2,3,8> schedule is the faster of the two 4-per-CU builds, so it is the default.  Tile rows
+  // are walked in groups of 4 (+0.5-1 %).
   static const int stages = getenv("GJ_GLDS_STAGES") ? atoi(getenv("GJ_GLDS_STAGES")) : 9;
   static const int group = getenv("GJ_GEMM_GROUP") ? atoi(getenv("GJ_GEMM_GROUP")) : 4;
   a.group = group;
@@ -629,9 +632,9 @@ static void launch(const GemmArgs& a, hipStream_t s) {
     return launch_cfg<T, AL, MODE, CfgSmall>(a, s);
   int v = gemm_variant();
   if (v == kAutoVariant) {
-    // Deep trailing updates (K >= 384) with enough 128x128 tiles to fill the chip: the big tile with
-    // two K slices in flight (fp64 57.6 vs 53.5 TF narrow at 32768x4096x512; fp32 the 64x64-per-wave
-    // square tile, 106.6 vs 97.5 TF).  Everything else keeps the 4-WG/CU narrow tile.
+    // Deep trailing updates (K >= 384) with enough 128x128 tiles to fill the chip: fp64 the LDS-DMA
+    // kernel (61 TF/s vs 57.6 register-staged at 32768x4096x512), fp32 the 64x64-per-wave square
+    // tile (110.5 TF/s).  Everything else keeps the register-staged narrow tile.
     const int64_t big_tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
     const bool deep = a.K >= 384 && big_tiles >= 512;
     v = !deep ? 1 : (sizeof(T) == 8 ? 11 : 6);
