@@ -45,6 +45,19 @@ struct GemmExtra {
   bool latency = false;
 };
 
+// One product of a batched small-GEMM launch (Device::gemm_batch): C (+)= A B, A K-major.
+struct GemmDesc {
+  GemmOp op = GemmOp::Acc;
+  int64_t M = 0, N = 0, K = 0;
+  const void* A = nullptr;
+  int64_t lda = 0;
+  const void* B = nullptr;
+  int64_t ldb = 0;
+  void* C = nullptr;
+  int64_t ldc = 0;
+  GemmExtra ex;
+};
+
 class Device {
  public:
   virtual ~Device() = default;
@@ -120,6 +133,16 @@ class Device {
   virtual void gemm(DType dt, GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const void* A,
                     int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int s,
                     const GemmExtra& ex = GemmExtra()) = 0;
+  // Independent small K-major GEMMs (the panel-piece products of one pivot step) as one launch
+  // where the device can; the default issues them one by one.
+  virtual void gemm_batch(DType dt, const GemmDesc* d, int n, int s) {
+    for (int i = 0; i < n; ++i) {
+      GemmExtra ex = d[i].ex;
+      ex.latency = true;
+      gemm(dt, d[i].op, ALayout::KMajor, d[i].M, d[i].N, d[i].K, d[i].A, d[i].lda, d[i].B, d[i].ldb,
+           d[i].C, d[i].ldc, s, ex);
+    }
+  }
   // Finalisation gather: dst[(dst_blk[b]*m + r)*ldd + c*m + j] = X[(b*m + r)*ldx + colsrc[c]*m + j]
   // for local block b < nblk, destination column block c < Nr.
   virtual void permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx,

@@ -62,6 +62,7 @@ class HipDevice : public Device {
   void gemm(DType dt, GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const void* A,
             int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int s,
             const GemmExtra& ex = GemmExtra()) override;
+  void gemm_batch(DType dt, const GemmDesc* d, int n, int s) override;
   void permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx, int64_t nblk,
                       int64_t m, int64_t Nr, const int32_t* dst_blk, const int32_t* colsrc,
                       int s) override;

@@ -150,8 +150,10 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
 }
 
+// One output tile of C (+)= A B (register-staged K slices, double-buffered LDS).  `tile` indexes the
+// tiles_m x tiles_n grid with the N tiles fastest (they share the A slab).
 template <typename T, int AL, int MODE, typename CF>
-__global__ __launch_bounds__(CF::NT, CF::WAVES_PER_SIMD) void gemm_kernel(GemmArgs g) {
+__device__ __forceinline__ void gemm_tile(const GemmArgs& g, const int tile) {
   using MF = Mfma<T>;
   using acc_t = typename MF::acc_t;
   constexpr int ES = sizeof(T);
@@ -160,9 +162,6 @@ __global__ __launch_bounds__(CF::NT, CF::WAVES_PER_SIMD) void gemm_kernel(GemmAr
   __shared__ T ldsA[2][BK][CF::LDA];  // K-major A slices (double-buffered)
   __shared__ T ldsB[2][BK][CF::LDB];  // B slices
 
-  const int nwg = g.tiles_m * g.tiles_n;
-  const int tile = xcd_remap((int)blockIdx.x, nwg);
-  // within an XCD's contiguous range, walk the N tiles fastest (they share the A slab)
   const int tm = tile / g.tiles_n, tn = tile % g.tiles_n;
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
 
@@ -354,6 +353,37 @@ __global__ __launch_bounds__(CF::NT, CF::WAVES_PER_SIMD) void gemm_kernel(GemmAr
         for (int off = 1; off < 16; off <<= 1) s += __shfl_xor(s, off, 64);
         if ((lane & 15) == 0 && row < g.M) g.partial[row * g.nparts + (int64_t)tn * WN + wn] = s;
       }
+  }
+}
+
+template <typename T, int AL, int MODE, typename CF>
+__global__ __launch_bounds__(CF::NT, CF::WAVES_PER_SIMD) void gemm_kernel(GemmArgs g) {
+  gemm_tile<T, AL, MODE, CF>(g, xcd_remap((int)blockIdx.x, g.tiles_m * g.tiles_n));
+}
+
+// Several independent small GEMMs in one launch (the panel-piece products of one pivot step): the
+// launch latency and the wait for a free CU slot are paid once instead of per product.  Workgroup
+// b works on tile b - start[i] of product i (start[] = prefix sums of the tile counts).  Every
+// product is C += A B with K-major A; C = A B is the same with all columns masked on input.
+constexpr int kMaxBatch = 4;
+struct GemmBatch {
+  GemmArgs a[kMaxBatch];
+  int start[kMaxBatch];
+  int n;
+};
+
+template <typename T, typename CF>
+__global__ __launch_bounds__(CF::NT, CF::WAVES_PER_SIMD) void gemm_batch_kernel(GemmBatch b) {
+  const int bid = (int)blockIdx.x;
+  int i = 0;
+#pragma unroll
+  for (int k = 1; k < kMaxBatch; ++k) i += (k < b.n && bid >= b.start[k]) ? 1 : 0;
+  // constant-index copies (a dynamically indexed kernel-argument array would go through scratch)
+  switch (i) {
+    case 0: gemm_tile<T, 1, MODE_ACC, CF>(b.a[0], bid - b.start[0]); break;
+    case 1: gemm_tile<T, 1, MODE_ACC, CF>(b.a[1], bid - b.start[1]); break;
+    case 2: gemm_tile<T, 1, MODE_ACC, CF>(b.a[2], bid - b.start[2]); break;
+    default: gemm_tile<T, 1, MODE_ACC, CF>(b.a[3], bid - b.start[3]); break;
   }
 }
 
@@ -694,6 +724,41 @@ void gemm(DType dt, int op, int a_kmajor, int64_t M, int64_t N, int64_t K, const
     GJ_DISPATCH(float)
   }
 #undef GJ_DISPATCH
+}
+
+void gemm_batch(DType dt, const GemmDesc* d, int n, hipStream_t s) {
+  using CF = CfgSmall;
+  GemmBatch b{};
+  int tiles = 0;
+  auto flush = [&]() {
+    if (b.n == 0) return;
+    for (int k = b.n; k < kMaxBatch; ++k) b.start[k] = tiles;
+    if (dt == DType::F64)
+      hipLaunchKernelGGL((gemm_batch_kernel<double, CF>), dim3((unsigned)tiles), dim3(CF::NT), 0, s, b);
+    else
+      hipLaunchKernelGGL((gemm_batch_kernel<float, CF>), dim3((unsigned)tiles), dim3(CF::NT), 0, s, b);
+    b = GemmBatch{};
+    tiles = 0;
+  };
+  for (int e = 0; e < n; ++e) {
+    const GemmDesc& g = d[e];
+    if (g.M <= 0 || g.N <= 0) continue;
+    GemmArgs& a = b.a[b.n];
+    a = GemmArgs{};
+    a.M = g.M; a.N = g.N; a.K = g.K; a.A = g.A; a.lda = g.lda; a.B = g.B; a.ldb = g.ldb; a.C = g.C;
+    a.ldc = g.ldc;
+    fill_extra(a, &g.ex);
+    if (g.op == GemmOp::Store) {  // every input column masked: C enters as 0 and is never read
+      a.zc0 = 0;
+      a.zc1 = g.N;
+    }
+    a.tiles_m = (int)((g.M + CF::BM - 1) / CF::BM);
+    a.tiles_n = (int)((g.N + CF::BN - 1) / CF::BN);
+    b.start[b.n++] = tiles;
+    tiles += a.tiles_m * a.tiles_n;
+    if (b.n == kMaxBatch) flush();
+  }
+  flush();
 }
 
 int residual_nparts(int64_t N) { return (int)(((N + CfgBig::BN - 1) / CfgBig::BN) * CfgBig::WN); }

@@ -11,6 +11,7 @@
 
 #include <cstring>
 #include <memory>
+#include <tuple>
 
 #include "gj/comms.hpp"
 #include "gj/engine.hpp"
@@ -165,6 +166,24 @@ PYBIND11_MODULE(_C, mod) {
            py::arg("A"), py::arg("lda"), py::arg("B"), py::arg("ldb"), py::arg("C"), py::arg("ldc"),
            py::arg("zc0") = 0, py::arg("zc1") = 0, py::arg("zero_rows") = std::vector<int64_t>(),
            py::arg("zh") = 0)
+      .def("gemm_batch",
+           [](Device& d, const std::string& dt,
+              const std::vector<std::tuple<std::string, int64_t, int64_t, int64_t, U, int64_t, U, int64_t,
+                                           U, int64_t>>& ps) {
+             std::vector<GemmDesc> v(ps.size());
+             for (size_t i = 0; i < ps.size(); ++i) {
+               const auto& t = ps[i];
+               GemmDesc& g = v[i];
+               g.op = std::get<0>(t) == "store" ? GemmOp::Store : GemmOp::Acc;
+               g.M = std::get<1>(t); g.N = std::get<2>(t); g.K = std::get<3>(t);
+               g.A = (const void*)std::get<4>(t); g.lda = std::get<5>(t);
+               g.B = (const void*)std::get<6>(t); g.ldb = std::get<7>(t);
+               g.C = (void*)std::get<8>(t); g.ldc = std::get<9>(t);
+             }
+             d.gemm_batch(parse_dtype(dt), v.data(), (int)v.size(), S_MAIN);
+             d.sync_stream(S_MAIN);
+           },
+           py::arg("dtype"), py::arg("products"))
       .def("generate",
            [lay](Device& d, const std::string& dt, U X, int64_t n, int64_t m, int64_t p, int64_t k,
                  const std::string& kind, uint64_t seed) {

@@ -241,6 +241,11 @@ void HipDevice::gemm(DType dt, GemmOp op, ALayout al, int64_t M, int64_t N, int6
              C, ldc, hs(streams_[s]), &ex);
   check_launch();
 }
+void HipDevice::gemm_batch(DType dt, const GemmDesc* d, int n, int s) {
+  if (n <= 0) return;
+  kern::gemm_batch(dt, d, n, hs(streams_[s]));
+  check_launch();
+}
 void HipDevice::permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx,
                                int64_t nblk, int64_t m, int64_t Nr, const int32_t* dst_blk,
                                const int32_t* colsrc, int s) {

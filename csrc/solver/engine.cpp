@@ -384,21 +384,33 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
     GemmExtra lat;
     lat.latency = true;
     if (owner) {
-      for (int64_t jc = 0; jc < q; ++jc) {
-        if (jc == j) continue;
-        void* rp = elem(RP_, jc * m);
-        if (jc < j) {  // earlier pivot column: sum over steps jc..j-1 only, no input
-          dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, m, (j - jc) * m,
-                    elem(Lrow_[par][j], jc * m * m), m, elem(PP_[par], jc * m * dm + jc * m), dm, rp,
-                    dm, S_SIDE, lat);
-        } else {  // later panel column: look-ahead value + all earlier steps
-          dev_.copy2d(rp, dm * es, elem(X_, sl * m * npad + (t0 + jc) * m), npad * es, m * es, m,
-                      S_SIDE);
-          if (j > 0)
-            dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, m, m, j * m, Lrow_[par][j], m,
-                      elem(PP_[par], jc * m), dm, rp, dm, S_SIDE, lat);
+      // RP = the pivot row over the panel's columns before normalisation, in one batched launch:
+      //   earlier pivot columns jc < j: the sum over steps jc..j-1 only (no input),
+      //   later panel columns jc > j (contiguous): look-ahead value + all earlier steps.
+      GemmDesc pr[kMaxDepth];
+      int np = 0;
+      for (int64_t jc = 0; jc < j; ++jc) {
+        GemmDesc& g = pr[np++];
+        g.op = GemmOp::Store;
+        g.M = m; g.N = m; g.K = (j - jc) * m;
+        g.A = elem(Lrow_[par][j], jc * m * m); g.lda = m;
+        g.B = elem(PP_[par], jc * m * dm + jc * m); g.ldb = dm;
+        g.C = elem(RP_, jc * m); g.ldc = dm;
+      }
+      if (j + 1 < q) {
+        const int64_t w = (q - j - 1) * m;
+        dev_.copy2d(elem(RP_, (j + 1) * m), dm * es, elem(X_, sl * m * npad + (t0 + j + 1) * m),
+                    npad * es, w * es, m, S_SIDE);
+        if (j > 0) {
+          GemmDesc& g = pr[np++];
+          g.op = GemmOp::Acc;
+          g.M = m; g.N = w; g.K = j * m;
+          g.A = Lrow_[par][j]; g.lda = m;
+          g.B = elem(PP_[par], (j + 1) * m); g.ldb = dm;
+          g.C = elem(RP_, (j + 1) * m); g.ldc = dm;
         }
       }
+      dev_.gemm_batch(opt_.dtype, pr, np, S_SIDE);
       dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, q * m, m, Ht_[par][j], m, RP_, dm, pp,
                 dm, S_SIDE, lat);
       dev_.h_block(opt_.dtype, elem(pp, j * m), dm, Ht_[par][j], m, S_SIDE);

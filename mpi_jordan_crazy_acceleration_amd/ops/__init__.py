@@ -50,6 +50,21 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, op: str = "acc", a_k
     return C
 
 
+def gemm_batch(products) -> None:
+    """Independent small products in one launch: each item is (op, At, B, C) with At = A^T (K x M),
+    op "acc" (C += A@B) or "store" (C = A@B).  All tensors share one dtype and device."""
+    if not products:
+        return
+    C0 = products[0][3]
+    descs = []
+    for op, At, B, C in products:
+        assert At.dtype == B.dtype == C.dtype == C0.dtype and At.stride(-1) == 1 and B.stride(-1) == 1
+        assert C.stride(-1) == 1
+        M, N = C.shape
+        descs.append((op, M, N, At.shape[0], _p(At), At.stride(0), _p(B), B.stride(0), _p(C), C.stride(0)))
+    device_for(C0).gemm_batch(_DT[C0.dtype], descs)
+
+
 def generate(X: torch.Tensor, n: int, m: int, p: int = 1, k: int = 0, kind: str = "absdiff", seed: int = 0) -> torch.Tensor:
     device_for(X).generate(_DT[X.dtype], _p(X), n, m, p, k, kind, seed)
     return X

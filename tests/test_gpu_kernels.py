@@ -156,3 +156,28 @@ def test_gemm_variants_elimination_extras(native, variant, M, N, K, dtype):
         assert (Cs.cpu().double() - A @ B).abs().max().item() < tol
     finally:
         native.set_gemm_variant("auto")
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("count", [1, 3, 4, 6])
+def test_gemm_batch_mixed_store_acc(dtype, count):
+    """Batched small products (one launch per 4): store and acc mixed, ragged shapes, views with
+    leading dimensions of a shared buffer (the panel-piece layout)."""
+    shapes = [(128, 128, 384), (128, 384, 256), (100, 70, 33), (128, 128, 128), (64, 200, 520), (1, 3, 5)]
+    big = _rand((130, 900), dtype, 40).cuda()  # every C is a column window of this buffer
+    ref = big.cpu().double().clone()
+    prods, col = [], 0
+    for i in range(count):
+        M, N, K = shapes[i]
+        At = _rand((K, M), dtype, 50 + i).cuda()
+        B = _rand((K, 2 * N), dtype, 60 + i).cuda()[:, :N]
+        op = "store" if i % 2 == 0 else "acc"
+        C = big[:M, col:col + N]
+        prod = At.cpu().double().t() @ B.cpu().double()
+        ref[:M, col:col + N] = prod if op == "store" else ref[:M, col:col + N] + prod
+        prods.append((op, At, B, C))
+        col += N
+        col = col % 600
+    ops.gemm_batch(prods)
+    tol = (1e-12 if dtype == torch.float64 else 2e-5) * 520
+    assert (big.cpu().double() - ref).abs().max().item() < tol

@@ -194,3 +194,20 @@ def test_rows_device_io_on_host_executor(native):
     eng.download_rows_device(out.ctypes.data, n + 5)
     assert np.abs(out[:, :n] - np.linalg.inv(A)).max() / np.abs(np.linalg.inv(A)).max() < 1e-10
     assert np.isnan(out[:, n:]).all()
+
+
+def test_host_gemm_batch_matches_torch():
+    import torch
+    from mpi_jordan_crazy_acceleration_amd import ops
+    g = torch.Generator().manual_seed(5)
+    prods, refs = [], []
+    for i, (M, N, K) in enumerate([(16, 16, 48), (16, 40, 32), (9, 7, 5)]):
+        At = torch.rand(K, M, generator=g, dtype=torch.float64)
+        B = torch.rand(K, N, generator=g, dtype=torch.float64)
+        C = torch.rand(M, N, generator=g, dtype=torch.float64)
+        op = "store" if i != 1 else "acc"
+        refs.append(At.t() @ B + (C if op == "acc" else 0))
+        prods.append((op, At, B, C))
+    ops.gemm_batch(prods)
+    for (_, _, _, C), r in zip(prods, refs):
+        assert (C - r).abs().max().item() < 1e-12
