@@ -19,7 +19,7 @@ def main(variants):
     for var in variants:
         C.set_block_inverse_variant(var)
         for m in (64, 128):
-            for nblk in (8, 32, 256):
+            for nblk in (8, 32, 64, 256):
                 for dt in (torch.float64, torch.float32):
                     Lt = torch.randn(m, nblk * m, dtype=dt, device="cuda")
                     n = nblk * m
