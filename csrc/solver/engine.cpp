@@ -73,7 +73,11 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   int rc = opt_.reserve_cus;
   if (const char* e = std::getenv("GJ_RESERVE_CUS")) rc = std::atoi(e);
   if (const char* e = std::getenv("GJ_RESERVE_MODE")) opt_.reserve_mode = std::atoi(e);
-  if (rc < 0) rc = 0;  // auto: off until measured otherwise
+  // auto: up to N = 16384 the pivot chain is the critical path and its block inverses only start
+  // on a CU no trailing-update workgroup occupies, so keep 32 CUs (1/8 of the chip) off the MAIN
+  // streams: N=8192 p=1 -12 %, emulated p=2/4/8 at N=16384 -10/-16/-14 %.  At N=32768 the GEMM is
+  // the critical path and the mask costs 4-10 % (profiles/cu_reserve_sweep.md).
+  if (rc < 0) rc = (dev_.on_gpu() && L_.npad <= 16384) ? 32 : 0;
   dev_.reserve_cus(rc, opt_.reserve_mode);
 }
 
