@@ -38,14 +38,12 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--chunk-cols", type=int, default=0)
     ap.add_argument("--depth", type=int, default=0,
-                    help="elimination steps fused per trailing update (0 = 2 up to N=8192, else 4: "
-                         "profiles/small_n_sweep.md)")
+                    help="elimination steps fused per trailing update (0 = the engine's choice: 2 up to "
+                         "N=8192, else 4, profiles/small_n_sweep.md)")
     ap.add_argument("--no-residual", action="store_true")
     ap.add_argument("--force-rccl", action="store_true", help="use the RCCL communicator even at 1 rank")
     ap.add_argument("--gemm-variant", default=None, help="big | narrow | tall (kernel tile config)")
     args = ap.parse_args()
-    if args.depth <= 0:
-        args.depth = 2 if args.n <= 8192 else 4
 
     # One hardware queue per stream: the engine's MAIN/SIDE/COMM streams plus torch's and RCCL's own
     # streams exceed HIP's default of 4, and streams that share a hardware queue also share its
@@ -137,7 +135,7 @@ def main() -> int:
                 "parallelism": f"block-row-cyclic p={world} (RCCL over xGMI)" if world > 1 else "single GPU",
                 "n": args.n,
                 "m": args.m,
-                "depth": args.depth,
+                "depth": eng.layout["depth"],
             },
             "solve_seconds_max": round(inner_max, 4),
             "residual_inf": res,

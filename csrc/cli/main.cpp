@@ -22,7 +22,7 @@
 //   --print-max N        corner size (reference MAX_P = 10)
 //   --eps E              singularity threshold factor (reference EPS = 1e-15)
 //   --chunk-cols C       broadcast pipelining granularity
-//   --depth D            elimination steps fused per trailing update (1..8, default 4)
+//   --depth D            elimination steps fused per trailing update (1..8; default: 2 up to N=8192, else 4)
 //   --repeat R           time R solves, report the last (min also in --json)
 //   --out FILE           write the inverse (text, or .bin)
 //   --rhs ones|random|FILE  also solve A x = b (x = inv(A) b) and report ||A x - b||_inf

@@ -38,7 +38,8 @@ namespace gj {
 struct SolveOptions {
   DType dtype = DType::F64;
   int64_t chunk_cols = 0;   // pipelining granularity of the pivot-row broadcast (0 = auto)
-  int depth = 4;            // elimination steps fused per trailing update (K = depth*m), 1..8
+  int depth = 0;            // elimination steps fused per trailing update (K = depth*m), 1..8;
+                            // 0 = auto: 2 up to N = 8192 (pivot-chain-bound), else 4
   double eps = kDefaultEps;
   bool sync_debug = false;  // synchronise every stream after every phase (race screening)
   bool profile = false;     // per-phase device timers (HIP events) + roctx ranges
@@ -119,6 +120,7 @@ class Engine {
   double axb_residual(const double* x, const double* b);
 
   int64_t real_local_rows() const;
+  int depth() const { return d_; }  // elimination steps per panel (after the auto choice)
 
  private:
   static constexpr int kMaxDepth = GemmExtra::kMaxZeroRows;

@@ -299,7 +299,7 @@ PYBIND11_MODULE(_C, mod) {
            }),
            py::arg("device"), py::arg("comm"), py::arg("n"), py::arg("m"), py::arg("dtype") = "fp64",
            py::arg("chunk_cols") = 0, py::arg("eps") = kDefaultEps, py::arg("sync_debug") = false,
-           py::arg("depth") = 4, py::arg("profile") = false, py::arg("comm_timeout_s") = 600.0)
+           py::arg("depth") = 0, py::arg("profile") = false, py::arg("comm_timeout_s") = 600.0)
       .def_property_readonly("layout",
                              [](PyEngine& e) {
                                const Layout& L = e.eng->layout();
@@ -307,6 +307,7 @@ PYBIND11_MODULE(_C, mod) {
                                d["n"] = L.n; d["m"] = L.m; d["p"] = L.p; d["k"] = L.k;
                                d["Nr"] = L.Nr; d["npad"] = L.npad; d["nblk"] = L.nblk;
                                d["rows"] = L.rows; d["real_rows"] = e.eng->real_local_rows();
+                               d["depth"] = e.eng->depth();
                                return d;
                              })
       .def("generate",

@@ -42,7 +42,7 @@ class GaussJordan:
     dtype: str = "fp64"
     comm: str = "auto"
     chunk_cols: int = 0
-    depth: int = 4
+    depth: int = 0  # 0 = auto (2 up to N=8192, else 4)
     eps: float = 1e-15
     sync_debug: bool = False
     residual: str = "always"

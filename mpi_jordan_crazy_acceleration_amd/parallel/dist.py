@@ -97,7 +97,7 @@ class DistributedGaussJordan:
 
     def __init__(self, n: int, m: int, dtype: str = "fp64", chunk_cols: int = 0, eps: float = 1e-15,
                  sync_debug: bool = False, host_threads: int = 0, local_rank: Optional[int] = None,
-                 depth: int = 4):
+                 depth: int = 0):
         C = load_native()
         if not dist.is_initialized():
             raise RuntimeError("torch.distributed is not initialised")
