@@ -136,7 +136,9 @@ def main() -> int:
                 "n": args.n,
                 "m": args.m,
                 "depth": eng.layout["depth"],
+                "bcast": eng.layout["bcast"],
             },
+            "bcast_tuning": comm.bcast_report(),
             "solve_seconds_max": round(inner_max, 4),
             "residual_inf": res,
             "status": st["status"],

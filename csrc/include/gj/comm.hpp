@@ -45,9 +45,27 @@ class Comm {
   virtual void group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) = 0;
   // Several broadcasts (any roots) issued as one group: RCCL runs them concurrently, so pivot rows
   // owned by different ranks travel over different xGMI links at the same time.
+  // Ops of at least direct_bcast_min() bytes take the two-round direct algorithm (bcast_direct).
   virtual void bcast_many(Device& dev, const std::vector<BcastOp>& ops, int s) {
-    for (const auto& o : ops) bcast(dev, o.buf, o.bytes, o.root, s);
+    std::vector<BcastOp> big;
+    for (const auto& o : ops)
+      if (use_direct(o.bytes)) big.push_back(o);
+      else bcast(dev, o.buf, o.bytes, o.root, s);
+    bcast_direct(dev, big, s);
   }
+
+  // Large-broadcast algorithm.  "ring" = the transport's own broadcast (RCCL:
+  // a pipelined chain per channel, so each hop forwards the whole message).  "direct" = the root
+  // sends 1/(p-1) of the message to every other rank over its own xGMI link, then the p-1 holders
+  // exchange their slices (two grouped point-to-point rounds; every link carries ~2/(p-1) of the
+  // message).  tune_bcast() sets it once per engine from GJ_BCAST=ring|direct|auto (default auto:
+  // on a GPU transport both are timed at the real segment size, checked for bit-exact delivery,
+  // and the faster is kept on every rank) and GJ_BCAST_MIN (smallest message sent direct, 1 MiB).
+  // Returns the chosen algorithm's name ("ring" at p <= 2: the two coincide).
+  std::string tune_bcast(Device& dev, size_t bytes);
+  size_t direct_bcast_min() const { return direct_min_; }
+  void set_direct_bcast_min(size_t b) { direct_min_ = b; }
+  const std::string& bcast_report() const { return bcast_report_; }
 
   // Host-blocking helpers (once-per-run agreement: errors, timings, residual maxima).
   virtual void barrier(Device& dev) = 0;
@@ -59,6 +77,14 @@ class Comm {
   // device-side collectives blocked on a dead peer return.
   virtual void check_health() {}
   virtual void abort() {}
+
+ protected:
+  // Whether GJ_BCAST=auto measures (a GPU transport whose two algorithms differ in cost).
+  virtual bool tunable() const { return false; }
+  bool use_direct(size_t bytes) const { return direct_min_ > 0 && size() > 2 && bytes >= direct_min_; }
+  void bcast_direct(Device& dev, const std::vector<BcastOp>& ops, int s);
+  size_t direct_min_ = 0;
+  std::string bcast_report_;
 };
 
 // A trivial single-rank communicator.

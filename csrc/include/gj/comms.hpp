@@ -38,6 +38,9 @@ class RcclComm : public Comm {
   void check_health() override;
   void abort() override;
 
+ protected:
+  bool tunable() const override { return true; }
+
  private:
   void* comm_for(int s) const;
   int n_ = 1, r_ = 0, device_ = 0;

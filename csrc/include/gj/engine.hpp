@@ -121,6 +121,7 @@ class Engine {
 
   int64_t real_local_rows() const;
   int depth() const { return d_; }  // elimination steps per panel (after the auto choice)
+  const std::string& bcast_algo() const { return bcast_algo_; }  // "ring" | "direct"
 
  private:
   static constexpr int kMaxDepth = GemmExtra::kMaxZeroRows;
@@ -164,6 +165,7 @@ class Engine {
   SolveOptions opt_;
   Layout L_;
   int d_ = 1;
+  std::string bcast_algo_ = "ring";
   double norm_a_ = -1;
 
   // chunk plan (block-column ranges, multiples of d_ blocks so a panel never straddles chunks)

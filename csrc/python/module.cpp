@@ -233,7 +233,8 @@ PYBIND11_MODULE(_C, mod) {
   py::class_<Comm, std::shared_ptr<Comm>>(mod, "Comm")
       .def_property_readonly("size", &Comm::size)
       .def_property_readonly("rank", &Comm::rank)
-      .def("describe", &Comm::describe);
+      .def("describe", &Comm::describe)
+      .def("bcast_report", &Comm::bcast_report);
   mod.def("self_comm", [] { return std::shared_ptr<Comm>(new SelfComm()); });
   mod.def("rccl_comm",
           [](std::vector<py::bytes> ids, int nranks, int rank, int device) {
@@ -308,6 +309,7 @@ PYBIND11_MODULE(_C, mod) {
                                d["Nr"] = L.Nr; d["npad"] = L.npad; d["nblk"] = L.nblk;
                                d["rows"] = L.rows; d["real_rows"] = e.eng->real_local_rows();
                                d["depth"] = e.eng->depth();
+                               d["bcast"] = e.eng->bcast_algo();
                                return d;
                              })
       .def("generate",

@@ -1,0 +1,139 @@
+// Transport-independent parts of Comm: the direct (scatter + exchange) broadcast and its tuner
+// ("benchmark both against ncclBroadcast").  The reference has one broadcast,
+// MPI_Bcast of the packed pivot row (main.cpp:1093-1097); on xGMI every GPU pair has its own link,
+// so a chain that forwards the whole row hop by hop leaves most links idle.
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "gj/comm.hpp"
+
+namespace gj {
+
+namespace {
+
+// Slice of the message held by rank j after round 1: the p-1 non-root ranks split it in 256-byte
+// aligned pieces (the last ones may be short or empty).
+void direct_slice(size_t bytes, int p, int root, int j, size_t& off, size_t& len) {
+  const int idx = j < root ? j : j - 1;
+  size_t q = (bytes + (size_t)(p - 2)) / (size_t)(p - 1);
+  q = (q + 255) & ~size_t(255);
+  off = std::min(bytes, q * (size_t)idx);
+  len = std::min(bytes, off + q) - off;
+}
+
+size_t env_size(const char* name, size_t dflt) {
+  const char* e = std::getenv(name);
+  if (!e || !*e) return dflt;
+  char* end = nullptr;
+  const unsigned long long v = std::strtoull(e, &end, 10);
+  GJ_REQUIRE(end && *end == '\0', std::string(name) + " must be a byte count");
+  return (size_t)v;
+}
+
+}  // namespace
+
+void Comm::bcast_direct(Device& dev, const std::vector<BcastOp>& ops, int s) {
+  if (ops.empty()) return;
+  const int p = size(), me = rank();
+  std::vector<P2POp> ph;
+  // round 1: the root hands slice j to rank j (p-1 links out of the root in parallel)
+  for (const auto& o : ops)
+    for (int j = 0; j < p; ++j) {
+      if (j == o.root || (me != o.root && me != j)) continue;
+      size_t off, len;
+      direct_slice(o.bytes, p, o.root, j, off, len);
+      if (len == 0) continue;
+      char* b = static_cast<char*>(o.buf) + off;
+      ph.push_back(me == o.root ? P2POp{b, len, j, true} : P2POp{b, len, o.root, false});
+    }
+  group_p2p(dev, ph, s);
+  // round 2: every non-root rank sends its slice to the other non-root ranks and receives theirs
+  // (per peer pair, sends and receives are issued in op order on both sides, so they match)
+  ph.clear();
+  for (const auto& o : ops) {
+    if (me == o.root) continue;
+    size_t off, len;
+    direct_slice(o.bytes, p, o.root, me, off, len);
+    char* b = static_cast<char*>(o.buf);
+    for (int k = 0; k < p; ++k) {
+      if (k == me || k == o.root) continue;
+      size_t ko, kl;
+      direct_slice(o.bytes, p, o.root, k, ko, kl);
+      if (len) ph.push_back(P2POp{b + off, len, k, true});
+      if (kl) ph.push_back(P2POp{b + ko, kl, k, false});
+    }
+  }
+  group_p2p(dev, ph, s);
+}
+
+std::string Comm::tune_bcast(Device& dev, size_t bytes) {
+  const char* e = std::getenv("GJ_BCAST");
+  const std::string mode = (e && *e) ? e : "auto";
+  GJ_REQUIRE(mode == "auto" || mode == "ring" || mode == "direct", "GJ_BCAST must be ring|direct|auto");
+  const size_t mn = std::max<size_t>(1, env_size("GJ_BCAST_MIN", size_t(1) << 20));
+  direct_min_ = 0;
+  if (size() <= 2 || mode == "ring") {
+    bcast_report_ = "ring";
+    return "ring";
+  }
+  if (mode == "direct") {
+    direct_min_ = mn;
+    bcast_report_ = "direct (GJ_BCAST)";
+    return "direct";
+  }
+  if (!tunable() || !dev.on_gpu() || bytes < mn) {
+    bcast_report_ = "ring";
+    return "ring";
+  }
+  // Measure both at the engine's segment size on the COMM stream, roots rotating.
+  const int p = size(), me = rank();
+  const int s = S_COMM;
+  void* buf = dev.alloc(bytes);
+  // bit-exact delivery check of the direct path (root 1, so the root's own slice index is skipped)
+  std::vector<uint32_t> pat(bytes / 4 + 1), got(bytes / 4 + 1);
+  for (size_t i = 0; i < pat.size(); ++i) pat[i] = (uint32_t)(i * 2654435761u) ^ 0x5bd1e995u;
+  const int vroot = 1 % p;
+  if (me == vroot) dev.copy(buf, pat.data(), bytes, s);
+  else dev.memset0(buf, bytes, s);
+  dev.sync_stream(s);
+  bcast_direct(dev, {BcastOp{buf, bytes, vroot}}, s);
+  dev.copy(got.data(), buf, bytes, s);
+  dev.sync_stream(s);
+  const bool ok_local = std::memcmp(got.data(), pat.data(), bytes) == 0;
+  const bool ok = host_max(dev, ok_local ? 0.0 : 1.0) == 0.0;
+  auto time_algo = [&](bool direct) {
+    auto run = [&](int it) {
+      const BcastOp o{buf, bytes, it % p};
+      if (direct) bcast_direct(dev, {o}, s);
+      else bcast(dev, o.buf, o.bytes, o.root, s);
+    };
+    for (int it = 0; it < 2; ++it) run(it);
+    dev.sync_stream(s);
+    host_max(dev, 0.0);  // barrier
+    const auto t0 = std::chrono::steady_clock::now();
+    const int iters = 2 * p;
+    for (int it = 0; it < iters; ++it) run(it);
+    dev.sync_stream(s);
+    const double ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / iters;
+    return host_max(dev, ms);
+  };
+  const double t_ring = time_algo(false);
+  const double t_direct = ok ? time_algo(true) : -1.0;
+  dev.release(buf);
+  const bool use = ok && t_direct < 0.95 * t_ring;
+  if (use) direct_min_ = mn;
+  char line[160];
+  std::snprintf(line, sizeof line, "%s (auto, %zu B: ring %.3f ms, direct %.3f ms%s)",
+                use ? "direct" : "ring", bytes, t_ring, t_direct, ok ? "" : ", direct FAILED check");
+  bcast_report_ = line;
+  return use ? "direct" : "ring";
+}
+
+}  // namespace gj

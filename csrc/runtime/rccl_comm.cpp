@@ -3,7 +3,9 @@
 //   M9  MPI_Allreduce(PivotMin, user op)  -> ncclAllGather of 32-B records (SIDE communicator)
 //   M10 MPI_Bcast(pivot row)              -> ncclBroadcast per column chunk and pivot row (COMM
 //                                            communicator), pipelined behind the trailing update;
-//                                            independent ones are issued as one group (bcast_many)
+//                                            independent ones are issued as one group (bcast_many);
+//                                            or, when Comm::tune_bcast measured it faster, the
+//                                            direct scatter + slice exchange (runtime/comm.cpp)
 //   M11 MPI_Send/Recv row swap            -> no per-step traffic; one grouped ncclSend/ncclRecv
 //                                            exchange at the end (finalize)
 //   M14 MPI_Sendrecv_replace ring (residual) -> ncclAllGather of the inverse strips
@@ -75,15 +77,20 @@ void RcclComm::allgather(Device& dev, const void* send, void* recv, size_t bytes
 
 void RcclComm::bcast(Device& dev, void* buf, size_t bytes, int root, int s) {
   if (n_ == 1) return;
+  if (use_direct(bytes)) return bcast_direct(dev, {BcastOp{buf, bytes, root}}, s);
   NCCL_OK(ncclBroadcast(buf, buf, bytes, ncclUint8, root, static_cast<ncclComm_t>(comm_for(s)), st(dev, s)));
 }
 
 void RcclComm::bcast_many(Device& dev, const std::vector<BcastOp>& ops, int s) {
   if (n_ == 1 || ops.empty()) return;
   ncclComm_t c = static_cast<ncclComm_t>(comm_for(s));
+  std::vector<BcastOp> big;
   NCCL_OK(ncclGroupStart());
-  for (const auto& o : ops) NCCL_OK(ncclBroadcast(o.buf, o.buf, o.bytes, ncclUint8, o.root, c, st(dev, s)));
+  for (const auto& o : ops)
+    if (use_direct(o.bytes)) big.push_back(o);
+    else NCCL_OK(ncclBroadcast(o.buf, o.buf, o.bytes, ncclUint8, o.root, c, st(dev, s)));
   NCCL_OK(ncclGroupEnd());
+  bcast_direct(dev, big, s);
 }
 
 void RcclComm::allreduce_max(Device& dev, double* buf, size_t count, int s) {

@@ -65,6 +65,13 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
     for (int64_t b = cb0_[c]; b < cb1_[c]; ++b) chunk_of_[b] = (int64_t)c;
 
   alloc_buffers();
+  // Broadcast algorithm for the pivot-row segments (m x chunk width): ring or direct, measured here
+  // on a GPU transport at p > 2 (Comm::tune_bcast; every rank takes the same decision).
+  {
+    int64_t wmax = 0;
+    for (size_t c = 0; c < cb0_.size(); ++c) wmax = std::max(wmax, chunk_w((int64_t)c));
+    bcast_algo_ = comm_.tune_bcast(dev_, (size_t)L_.m * wmax * esz());
+  }
   // Two trailing-update streams (GJ_TWO_MAIN_STREAMS=1): measured slower — N=32768 1283 vs 1167 ms,
   // p=8 emulation 0.191 vs 0.166 s (two concurrent GEMMs interleave their tiles, lose L2 locality
   // and crowd out the pivot path) — so off by default.
@@ -422,7 +429,7 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
                 dm, S_SIDE, lat);
       dev_.h_block(opt_.dtype, elem(pp, j * m), dm, Ht_[par][j], m, S_SIDE);
     }
-    comm_.bcast(dev_, pp, (size_t)m * dm * es, r.owner, S_SIDE);
+    comm_.bcast_many(dev_, {BcastOp{pp, (size_t)m * dm * es, r.owner}}, S_SIDE);
     prof_end(PH_PIECES, pe, S_SIDE);
     dev_.record(ev_pp_[par][j], S_SIDE);
     dbg_sync();

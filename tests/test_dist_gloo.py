@@ -79,3 +79,18 @@ def test_gloo_distributed_inverse(world, n, m, depth, kind):
         assert np.allclose(corner, ref[:4, :4], rtol=1e-8, atol=1e-10)
     inv = out[0][3]
     assert np.abs(inv - ref).max() / np.abs(ref).max() < 1e-9
+
+
+def test_gloo_direct_bcast(monkeypatch):
+    # the direct broadcast's two grouped point-to-point rounds over real processes (spawned ranks
+    # inherit the environment): torch.distributed isend/irecv here, ncclSend/ncclRecv on xGMI
+    from mpi_jordan_crazy_acceleration_amd.utils import generate_matrix
+
+    monkeypatch.setenv("GJ_BCAST", "direct")
+    monkeypatch.setenv("GJ_BCAST_MIN", "1")
+    n = 50
+    out = _run(4, n, 6, 2, "file")
+    ref = np.linalg.inv(generate_matrix(n, "random", 11))
+    for rank, status, res, inv, corner in out:
+        assert status == 0 and res < 1e-8, (status, res)
+    assert np.abs(out[0][3] - ref).max() / np.abs(ref).max() < 1e-9
