@@ -143,3 +143,19 @@ def test_two_main_streams_option(native, monkeypatch):
     assert eng.solve()["status"] == 0
     ref = np.linalg.inv(A)
     assert np.abs(eng.download_local_rows() - ref).max() / np.abs(ref).max() < 1e-8
+
+
+@pytest.mark.parametrize("p", [3, 8])
+def test_direct_bcast_loopback_ranks_on_one_gpu(p, monkeypatch):
+    # the direct broadcast's grouped point-to-point rounds with device buffers, streams and events
+    # (loopback virtual ranks on the GPU); bit-identical to the ring path
+    n, m = 700, 64
+    A = generate_matrix(n, "random", 9)[::-1].copy()
+    monkeypatch.setenv("GJ_BCAST", "ring")
+    ring = gj.GaussJordan(block_size=m, ranks=p, device="gpu", comm="loopback", depth=2, chunk_cols=128).inverse(A)
+    monkeypatch.setenv("GJ_BCAST", "direct")
+    monkeypatch.setenv("GJ_BCAST_MIN", "1")
+    direct = gj.GaussJordan(block_size=m, ranks=p, device="gpu", comm="loopback", depth=2, chunk_cols=128).inverse(A)
+    assert np.array_equal(ring, direct)
+    ref = np.linalg.inv(A)
+    assert np.abs(direct - ref).max() / np.abs(ref).max() < 1e-8
