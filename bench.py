@@ -42,6 +42,9 @@ def main() -> int:
                          "N=8192, else 4, profiles/small_n_sweep.md)")
     ap.add_argument("--no-residual", action="store_true")
     ap.add_argument("--force-rccl", action="store_true", help="use the RCCL communicator even at 1 rank")
+    ap.add_argument("--bcast", choices=["auto", "ring", "direct"], default=None,
+                    help="pivot-row broadcast at p > 2 (default: GJ_BCAST or auto = both timed at "
+                         "engine setup, the faster kept)")
     ap.add_argument("--gemm-variant", default=None, help="big | narrow | tall (kernel tile config)")
     args = ap.parse_args()
 
@@ -50,6 +53,8 @@ def main() -> int:
     # in-order barrier packets (a cross-stream event wait then stalls unrelated work).  Must be set
     # before the first HIP call of the process.
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    if args.bcast:
+        os.environ["GJ_BCAST"] = args.bcast
     import torch
     import torch.distributed as dist
 

@@ -28,6 +28,8 @@
 //   --rhs ones|random|FILE  also solve A x = b (x = inv(A) b) and report ||A x - b||_inf
 //   --out-x FILE         write x (text, or .bin); implies --rhs ones unless --rhs is given
 //   --json               machine-readable report on stderr
+//   --bcast auto|ring|direct  pivot-row broadcast algorithm at p > 2 (sets GJ_BCAST; auto = timed
+//                        against each other at startup, Comm::tune_bcast)
 //   --sync-debug         synchronise after every phase (race screening)
 //   --profile            per-phase device timers (in --json) + roctx ranges for rocprofv3
 //   --comm-timeout S     seconds a rank waits for a pivot before declaring a peer failure
@@ -129,6 +131,11 @@ int main(int argc, char* argv[]) {
       else if (a == "--rhs") cfg.rhs = val("--rhs");
       else if (a == "--out-x") x_file = val("--out-x");
       else if (a == "--json") json = true;
+      else if (a == "--bcast") {
+        const std::string b = val("--bcast");
+        if (b != "auto" && b != "ring" && b != "direct") return usage(argv[0]);
+        setenv("GJ_BCAST", b.c_str(), 1);
+      }
       else if (a == "--sync-debug") cfg.solve.sync_debug = true;
       else if (a == "--profile") cfg.solve.profile = true;
       else if (a == "--comm-timeout") cfg.solve.comm_timeout_s = std::atof(val("--comm-timeout"));

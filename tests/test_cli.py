@@ -144,3 +144,22 @@ def test_profile_json_phases(gj_bin):
     assert set(ph) == {"column", "pivot_search", "pivot_exchange", "owner_edits", "panel_pieces",
                        "normalise_rows", "row_bcast", "trailing_update", "finalize"}
     assert ph["trailing_update"] > 0
+
+
+@pytest.mark.parametrize("mode", ["ring", "direct"])
+def test_bcast_flag(gj_bin, mode):
+    # 4 virtual host ranks; every broadcast takes the chosen algorithm (GJ_BCAST_MIN=1 -> direct for
+    # all sizes); the answer does not depend on it
+    import os
+    import subprocess
+
+    env = dict(os.environ, GJ_BCAST_MIN="1")
+    p = subprocess.run([str(gj_bin), "--device", "cpu", "--gpus", "4", "--bcast", mode, "--gen", "random",
+                        "--residual", "always", "40", "6"], capture_output=True, text=True, env=env, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert float(p.stdout.strip().split("\n")[-1].split()[-1]) < 1e-10
+
+
+def test_bcast_flag_rejects_unknown(gj_bin):
+    rc, out, _ = run(gj_bin, "--bcast", "tree", 10, 3)
+    assert rc == 1
