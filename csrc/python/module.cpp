@@ -234,7 +234,14 @@ PYBIND11_MODULE(_C, mod) {
       .def_property_readonly("size", &Comm::size)
       .def_property_readonly("rank", &Comm::rank)
       .def("describe", &Comm::describe)
-      .def("bcast_report", &Comm::bcast_report);
+      .def("bcast_report", &Comm::bcast_report)
+      .def("tune_bcast",
+           [](Comm& c, std::shared_ptr<Device> dev, size_t bytes) {
+             py::gil_scoped_release r;
+             c.tune_bcast(*dev, bytes);
+             return c.bcast_report();
+           },
+           py::arg("device"), py::arg("bytes"));
   mod.def("self_comm", [] { return std::shared_ptr<Comm>(new SelfComm()); });
   mod.def("rccl_comm",
           [](std::vector<py::bytes> ids, int nranks, int rank, int device) {

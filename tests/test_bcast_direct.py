@@ -49,3 +49,11 @@ def test_auto_mode_stays_ring_off_gpu(monkeypatch):
     C = gj.load_native()
     eng = C.Engine(C.host_device(2), C.self_comm(), 16, 4, "fp64")
     assert eng.layout["bcast"] == "ring"
+
+
+def test_tune_bcast_binding_single_rank(monkeypatch):
+    monkeypatch.setenv("GJ_BCAST", "auto")
+    C = gj.load_native()
+    comm = C.self_comm()
+    assert comm.tune_bcast(C.host_device(1), 1 << 20) == "ring"
+    assert comm.bcast_report() == "ring"
