@@ -154,13 +154,15 @@ void h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, hipStrea
 }
 
 // ---------------------------------------------------------------- pivot selection
-__global__ __launch_bounds__(256) void pivot_local_kernel(const double* scores, const int32_t* valid,
-                                                          const int32_t* used, const int32_t* pos,
-                                                          int64_t nblk, int64_t p, int64_t k,
-                                                          PivotRec* out) {
-  __shared__ PivotRec sh[256];
+// One wave: each lane scans every 64th candidate, then a 6-step shuffle tree (no LDS, no
+// workgroup barrier: this launch sits on the pivot chain once per step).  pivot_better is a strict
+// total order on valid records (distinct logical rows), so the tree shape cannot change the winner.
+__global__ __launch_bounds__(64) void pivot_local_kernel(const double* scores, const int32_t* valid,
+                                                         const int32_t* used, const int32_t* pos,
+                                                         int64_t nblk, int64_t p, int64_t k,
+                                                         PivotRec* out) {
   PivotRec best = pivot_invalid();
-  for (int64_t b = threadIdx.x; b < nblk; b += 256) {
+  for (int64_t b = threadIdx.x; b < nblk; b += 64) {
     const int64_t g = b * p + k;
     if (used[g] || !valid[b]) continue;
     PivotRec c;
@@ -171,21 +173,22 @@ __global__ __launch_bounds__(256) void pivot_local_kernel(const double* scores, 
     c.pad_ = 0;
     if (pivot_better(c, best, (int32_t)p)) best = c;
   }
-  sh[threadIdx.x] = best;
-  __syncthreads();
-  for (int off = 128; off >= 1; off >>= 1) {
-    if ((int)threadIdx.x < off) {
-      const PivotRec o = sh[threadIdx.x + off];
-      if (pivot_better(o, sh[threadIdx.x], (int32_t)p)) sh[threadIdx.x] = o;
-    }
-    __syncthreads();
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    PivotRec o;
+    o.score = __shfl_xor(best.score, off, 64);
+    o.logical = __shfl_xor(best.logical, off, 64);
+    o.phys = __shfl_xor(best.phys, off, 64);
+    o.valid = __shfl_xor(best.valid, off, 64);
+    o.pad_ = 0;
+    if (pivot_better(o, best, (int32_t)p)) best = o;
   }
-  if (threadIdx.x == 0) *out = sh[0];
+  if (threadIdx.x == 0) *out = best;
 }
 
 void pivot_local(const double* scores, const int32_t* valid, const int32_t* used, const int32_t* pos,
                  const Layout& L, PivotRec* out, hipStream_t s) {
-  hipLaunchKernelGGL(pivot_local_kernel, dim3(1), dim3(256), 0, s, scores, valid, used, pos, L.nblk,
+  hipLaunchKernelGGL(pivot_local_kernel, dim3(1), dim3(64), 0, s, scores, valid, used, pos, L.nblk,
                      L.p, L.k, out);
 }
 
