@@ -59,10 +59,13 @@ class Comm {
   // sends 1/(p-1) of the message to every other rank over its own xGMI link, then the p-1 holders
   // exchange their slices (two grouped point-to-point rounds; every link carries ~2/(p-1) of the
   // message).  tune_bcast() sets it once per engine from GJ_BCAST=ring|direct|auto (default auto:
-  // on a GPU transport both are timed at the real segment size, checked for bit-exact delivery,
-  // and the faster is kept on every rank) and GJ_BCAST_MIN (smallest message sent direct, 1 MiB).
+  // on a GPU transport both are timed at the real message sizes, checked for bit-exact delivery,
+  // and the faster is kept on every rank) and GJ_BCAST_MIN (smallest message measured / sent direct, 64 KiB).
   // Returns the chosen algorithm's name ("ring" at p <= 2: the two coincide).
   std::string tune_bcast(Device& dev, size_t bytes);
+  // Several message sizes: direct from the smallest measured size at which it wins there and at
+  // every larger one (the engine passes its panel-piece and row-segment sizes).
+  std::string tune_bcast(Device& dev, std::vector<size_t> sizes);
   size_t direct_bcast_min() const { return direct_min_; }
   void set_direct_bcast_min(size_t b) { direct_min_ = b; }
   const std::string& bcast_report() const { return bcast_report_; }

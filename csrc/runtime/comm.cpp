@@ -72,11 +72,13 @@ void Comm::bcast_direct(Device& dev, const std::vector<BcastOp>& ops, int s) {
   group_p2p(dev, ph, s);
 }
 
-std::string Comm::tune_bcast(Device& dev, size_t bytes) {
+std::string Comm::tune_bcast(Device& dev, size_t bytes) { return tune_bcast(dev, std::vector<size_t>{bytes}); }
+
+std::string Comm::tune_bcast(Device& dev, std::vector<size_t> sizes) {
   const char* e = std::getenv("GJ_BCAST");
   const std::string mode = (e && *e) ? e : "auto";
   GJ_REQUIRE(mode == "auto" || mode == "ring" || mode == "direct", "GJ_BCAST must be ring|direct|auto");
-  const size_t mn = std::max<size_t>(1, env_size("GJ_BCAST_MIN", size_t(1) << 20));
+  const size_t mn = std::max<size_t>(1, env_size("GJ_BCAST_MIN", size_t(64) << 10));
   direct_min_ = 0;
   if (size() <= 2 || mode == "ring") {
     bcast_report_ = "ring";
@@ -87,27 +89,31 @@ std::string Comm::tune_bcast(Device& dev, size_t bytes) {
     bcast_report_ = "direct (GJ_BCAST)";
     return "direct";
   }
-  if (!tunable() || !dev.on_gpu() || bytes < mn) {
+  std::sort(sizes.begin(), sizes.end());
+  sizes.erase(std::unique(sizes.begin(), sizes.end()), sizes.end());
+  sizes.erase(std::remove_if(sizes.begin(), sizes.end(), [&](size_t b) { return b < mn; }), sizes.end());
+  if (!tunable() || !dev.on_gpu() || sizes.empty()) {
     bcast_report_ = "ring";
     return "ring";
   }
-  // Measure both at the engine's segment size on the COMM stream, roots rotating.
+  // Measure both at the engine's message sizes on the COMM stream, roots rotating.
   const int p = size(), me = rank();
   const int s = S_COMM;
-  void* buf = dev.alloc(bytes);
+  const size_t maxb = sizes.back();
+  void* buf = dev.alloc(maxb);
   // bit-exact delivery check of the direct path (root 1, so the root's own slice index is skipped)
-  std::vector<uint32_t> pat(bytes / 4 + 1), got(bytes / 4 + 1);
+  std::vector<uint32_t> pat(maxb / 4 + 1), got(maxb / 4 + 1);
   for (size_t i = 0; i < pat.size(); ++i) pat[i] = (uint32_t)(i * 2654435761u) ^ 0x5bd1e995u;
   const int vroot = 1 % p;
-  if (me == vroot) dev.copy(buf, pat.data(), bytes, s);
-  else dev.memset0(buf, bytes, s);
+  if (me == vroot) dev.copy(buf, pat.data(), maxb, s);
+  else dev.memset0(buf, maxb, s);
   dev.sync_stream(s);
-  bcast_direct(dev, {BcastOp{buf, bytes, vroot}}, s);
-  dev.copy(got.data(), buf, bytes, s);
+  bcast_direct(dev, {BcastOp{buf, maxb, vroot}}, s);
+  dev.copy(got.data(), buf, maxb, s);
   dev.sync_stream(s);
-  const bool ok_local = std::memcmp(got.data(), pat.data(), bytes) == 0;
+  const bool ok_local = std::memcmp(got.data(), pat.data(), maxb) == 0;
   const bool ok = host_max(dev, ok_local ? 0.0 : 1.0) == 0.0;
-  auto time_algo = [&](bool direct) {
+  auto time_algo = [&](bool direct, size_t bytes) {
     auto run = [&](int it) {
       const BcastOp o{buf, bytes, it % p};
       if (direct) bcast_direct(dev, {o}, s);
@@ -124,16 +130,31 @@ std::string Comm::tune_bcast(Device& dev, size_t bytes) {
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / iters;
     return host_max(dev, ms);
   };
-  const double t_ring = time_algo(false);
-  const double t_direct = ok ? time_algo(true) : -1.0;
+  // direct from the smallest measured size at which it wins at that and every larger size
+  std::string detail;
+  size_t thr = 0;
+  bool wins_above = true;
+  std::vector<bool> win(sizes.size());
+  std::vector<double> tr(sizes.size()), td(sizes.size());
+  for (size_t i = 0; i < sizes.size(); ++i) {
+    tr[i] = time_algo(false, sizes[i]);
+    td[i] = ok ? time_algo(true, sizes[i]) : -1.0;
+    win[i] = ok && td[i] < 0.95 * tr[i];
+  }
+  for (size_t i = sizes.size(); i-- > 0;) {
+    wins_above = wins_above && win[i];
+    if (wins_above) thr = sizes[i];
+  }
   dev.release(buf);
-  const bool use = ok && t_direct < 0.95 * t_ring;
-  if (use) direct_min_ = mn;
-  char line[160];
-  std::snprintf(line, sizeof line, "%s (auto, %zu B: ring %.3f ms, direct %.3f ms%s)",
-                use ? "direct" : "ring", bytes, t_ring, t_direct, ok ? "" : ", direct FAILED check");
-  bcast_report_ = line;
-  return use ? "direct" : "ring";
+  direct_min_ = thr;
+  for (size_t i = 0; i < sizes.size(); ++i) {
+    char line[128];
+    std::snprintf(line, sizeof line, "%s%zu B: ring %.3f ms, direct %.3f ms", i ? "; " : "", sizes[i], tr[i], td[i]);
+    detail += line;
+  }
+  const std::string choice = thr == 0 ? "ring" : (thr == sizes.front() ? "direct" : "direct from " + std::to_string(thr) + " B");
+  bcast_report_ = choice + " (auto: " + detail + (ok ? "" : "; direct FAILED check") + ")";
+  return thr == 0 ? "ring" : "direct";
 }
 
 }  // namespace gj

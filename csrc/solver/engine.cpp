@@ -65,12 +65,14 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
     for (int64_t b = cb0_[c]; b < cb1_[c]; ++b) chunk_of_[b] = (int64_t)c;
 
   alloc_buffers();
-  // Broadcast algorithm for the pivot-row segments (m x chunk width): ring or direct, measured here
+  // Broadcast algorithm for the panel pieces (m x d*m) and the pivot-row segments (m x chunk width):
+  // ring or direct, measured here
   // on a GPU transport at p > 2 (Comm::tune_bcast; every rank takes the same decision).
   {
     int64_t wmax = 0;
     for (size_t c = 0; c < cb0_.size(); ++c) wmax = std::max(wmax, chunk_w((int64_t)c));
-    bcast_algo_ = comm_.tune_bcast(dev_, (size_t)L_.m * wmax * esz());
+    const size_t pp_bytes = (size_t)L_.m * d_ * L_.m * esz();  // panel piece (SIDE, pivot chain)
+    bcast_algo_ = comm_.tune_bcast(dev_, std::vector<size_t>{pp_bytes, (size_t)L_.m * wmax * esz()});
   }
   // Two trailing-update streams (GJ_TWO_MAIN_STREAMS=1): measured slower — N=32768 1283 vs 1167 ms,
   // p=8 emulation 0.191 vs 0.166 s (two concurrent GEMMs interleave their tiles, lose L2 locality
