@@ -53,6 +53,9 @@ def main() -> int:
     # in-order barrier packets (a cross-stream event wait then stalls unrelated work).  Must be set
     # before the first HIP call of the process.
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    # Kernel arguments in device memory: measured 0 vs 1 on one box, N = 8192 31.3 vs 30.2 ms
+    # (profiles/small_n_sweep.md); pinned in case a runtime's default differs.
+    os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
     if args.bcast:
         os.environ["GJ_BCAST"] = args.bcast
     import torch
