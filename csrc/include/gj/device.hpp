@@ -121,6 +121,15 @@ class Device {
   virtual void pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos,
                             int32_t* phys_at, int32_t* used, int32_t* seq, PivotResult* out,
                             PivotResult* host_out, int s) = 0;
+  // One rank (p == 1): pivot_local + pivot_global as one launch (the record all-gather is skipped
+  // there, so the two were back to back on the pivot chain).  Default: the two calls.
+  virtual void pivot_select_single(const double* scores, const int32_t* valid, const Layout& L,
+                                   int32_t t, int32_t* pos, int32_t* phys_at, int32_t* used,
+                                   int32_t* seq, PivotRec* rec, PivotResult* out,
+                                   PivotResult* host_out, int s) {
+    pivot_local(scores, valid, used, pos, L, rec, s);
+    pivot_global(rec, 1, t, pos, phys_at, used, seq, out, host_out, s);
+  }
   // Owner-side edits of a pivot step, fused (one launch): for the pivot's local block row b0 (rows
   // row0 .. row0+m-1 of the K-major multiplier panel At, ld ldl) save the multipliers of the panel's
   // earlier steps, lrow[k*m + c] = At[k*ldl + row0 + c] for k < j*m, then set those rows of At to

@@ -53,6 +53,9 @@ class HipDevice : public Device {
                      int s) override;
   void pivot_local(const double* scores, const int32_t* valid, const int32_t* used,
                    const int32_t* pos, const Layout& L, PivotRec* out, int s) override;
+  void pivot_select_single(const double* scores, const int32_t* valid, const Layout& L, int32_t t,
+                           int32_t* pos, int32_t* phys_at, int32_t* used, int32_t* seq, PivotRec* rec,
+                           PivotResult* out, PivotResult* host_out, int s) override;
   void pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos, int32_t* phys_at,
                     int32_t* used, int32_t* seq, PivotResult* out, PivotResult* host_out,
                     int s) override;

@@ -46,6 +46,9 @@ void extract_neg_t(DType dt, void* Lt, int64_t ldl, const void* X, int64_t ldx, 
 void add_diag(DType dt, void* A, int64_t ld, int64_t nd, double alpha, hipStream_t s);
 void pivot_local(const double* scores, const int32_t* valid, const int32_t* used, const int32_t* pos,
                  const Layout& L, PivotRec* out, hipStream_t s);
+void pivot_select_single(const double* scores, const int32_t* valid, const Layout& L, int32_t t,
+                         int32_t* pos, int32_t* phys_at, int32_t* used, int32_t* seq, PivotRec* rec,
+                         PivotResult* out, PivotResult* host_out, hipStream_t s);
 void pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos, int32_t* phys_at,
                   int32_t* used, int32_t* seq, PivotResult* out, PivotResult* host_out, hipStream_t s);
 void owner_edits(DType dt, void* At, int64_t ldl, int64_t row0, int64_t j, int64_t m, void* lrow,

@@ -157,10 +157,8 @@ void h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, hipStrea
 // One wave: each lane scans every 64th candidate, then a 6-step shuffle tree (no LDS, no
 // workgroup barrier: this launch sits on the pivot chain once per step).  pivot_better is a strict
 // total order on valid records (distinct logical rows), so the tree shape cannot change the winner.
-__global__ __launch_bounds__(64) void pivot_local_kernel(const double* scores, const int32_t* valid,
-                                                         const int32_t* used, const int32_t* pos,
-                                                         int64_t nblk, int64_t p, int64_t k,
-                                                         PivotRec* out) {
+__device__ PivotRec pivot_local_wave(const double* scores, const int32_t* valid, const int32_t* used,
+                                     const int32_t* pos, int64_t nblk, int64_t p, int64_t k) {
   PivotRec best = pivot_invalid();
   for (int64_t b = threadIdx.x; b < nblk; b += 64) {
     const int64_t g = b * p + k;
@@ -183,6 +181,14 @@ __global__ __launch_bounds__(64) void pivot_local_kernel(const double* scores, c
     o.pad_ = 0;
     if (pivot_better(o, best, (int32_t)p)) best = o;
   }
+  return best;
+}
+
+__global__ __launch_bounds__(64) void pivot_local_kernel(const double* scores, const int32_t* valid,
+                                                         const int32_t* used, const int32_t* pos,
+                                                         int64_t nblk, int64_t p, int64_t k,
+                                                         PivotRec* out) {
+  const PivotRec best = pivot_local_wave(scores, valid, used, pos, nblk, p, k);
   if (threadIdx.x == 0) *out = best;
 }
 
@@ -192,13 +198,9 @@ void pivot_local(const double* scores, const int32_t* valid, const int32_t* used
                      L.p, L.k, out);
 }
 
-__global__ void pivot_global_kernel(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos,
-                                    int32_t* phys_at, int32_t* used, int32_t* seq, PivotResult* out,
-                                    PivotResult* host_out) {
-  if (threadIdx.x != 0) return;
-  PivotRec best = pivot_invalid();
-  for (int32_t q = 0; q < p; ++q)
-    if (pivot_better(recs[q], best, p)) best = recs[q];
+// Winner of the gathered records -> book-keeping, *out, and the host mirror (one thread).
+__device__ void pivot_finish(PivotRec best, int32_t p, int32_t t, int32_t* pos, int32_t* phys_at,
+                             int32_t* used, int32_t* seq, PivotResult* out, PivotResult* host_out) {
   PivotResult r;
   r.step = t;
   r.pad_ = 0;
@@ -228,6 +230,34 @@ __global__ void pivot_global_kernel(const PivotRec* recs, int32_t p, int32_t t, 
     h->step = r.step;
     __threadfence_system();
   }
+}
+
+__global__ void pivot_global_kernel(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos,
+                                    int32_t* phys_at, int32_t* used, int32_t* seq, PivotResult* out,
+                                    PivotResult* host_out) {
+  if (threadIdx.x != 0) return;
+  PivotRec best = pivot_invalid();
+  for (int32_t q = 0; q < p; ++q)
+    if (pivot_better(recs[q], best, p)) best = recs[q];
+  pivot_finish(best, p, t, pos, phys_at, used, seq, out, host_out);
+}
+
+// p == 1: local argmin and global book-keeping in one launch (the rank's record is the gathered set).
+__global__ __launch_bounds__(64) void pivot_select_single_kernel(
+    const double* scores, const int32_t* valid, int64_t nblk, int32_t t, int32_t* pos,
+    int32_t* phys_at, int32_t* used, int32_t* seq, PivotRec* rec, PivotResult* out,
+    PivotResult* host_out) {
+  const PivotRec best = pivot_local_wave(scores, valid, used, pos, nblk, 1, 0);
+  if (threadIdx.x != 0) return;
+  *rec = best;
+  pivot_finish(best, 1, t, pos, phys_at, used, seq, out, host_out);
+}
+
+void pivot_select_single(const double* scores, const int32_t* valid, const Layout& L, int32_t t,
+                         int32_t* pos, int32_t* phys_at, int32_t* used, int32_t* seq, PivotRec* rec,
+                         PivotResult* out, PivotResult* host_out, hipStream_t s) {
+  hipLaunchKernelGGL(pivot_select_single_kernel, dim3(1), dim3(64), 0, s, scores, valid, L.nblk, t, pos,
+                     phys_at, used, seq, rec, out, host_out);
 }
 
 void pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos, int32_t* phys_at,

@@ -219,6 +219,14 @@ void HipDevice::pivot_local(const double* scores, const int32_t* valid, const in
   kern::pivot_local(scores, valid, used, pos, L, out, hs(streams_[s]));
   check_launch();
 }
+void HipDevice::pivot_select_single(const double* scores, const int32_t* valid, const Layout& L,
+                                    int32_t t, int32_t* pos, int32_t* phys_at, int32_t* used,
+                                    int32_t* seq, PivotRec* rec, PivotResult* out,
+                                    PivotResult* host_out, int s) {
+  kern::pivot_select_single(scores, valid, L, t, pos, phys_at, used, seq, rec, out, host_out,
+                            hs(streams_[s]));
+  check_launch();
+}
 void HipDevice::pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos,
                              int32_t* phys_at, int32_t* used, int32_t* seq, PivotResult* out,
                              PivotResult* host_out, int s) {

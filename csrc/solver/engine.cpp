@@ -317,16 +317,23 @@ void Engine::select(int64_t t, const void* Lt) {
   int pe = prof_begin(S_SIDE);
   if (L_.nblk > 0)
     dev_.block_inverse(opt_.dtype, Lt, L_.rows, inv_, scores_, valid_, used_, L_, thresh, S_SIDE);
-  dev_.pivot_local(scores_, valid_, used_, pos_, L_, myrec_, S_SIDE);
-  prof_end(PH_PIVOT, pe, S_SIDE);
-  pe = prof_begin(S_SIDE);
-  // one rank: the local record is the gathered set (no copy launch on the critical path)
-  if (L_.p > 1) comm_.allgather(dev_, myrec_, recs_, sizeof(PivotRec), S_SIDE);
-  // the result goes straight to pinned host memory (no copy kernel); the host polls its step field
-  piv_host_[par].step = -1;
-  dev_.pivot_global(L_.p > 1 ? recs_ : myrec_, (int32_t)L_.p, (int32_t)t, pos_, phys_at_, used_, seq_,
-                    piv_dev_, &piv_host_[par], S_SIDE);
-  prof_end(PH_EXCHANGE, pe, S_SIDE);
+  if (L_.p == 1) {
+    // one rank: the local record is the gathered set -> local argmin + book-keeping in one launch;
+    // the result goes straight to pinned host memory (no copy kernel), the host polls its step field
+    piv_host_[par].step = -1;
+    dev_.pivot_select_single(scores_, valid_, L_, (int32_t)t, pos_, phys_at_, used_, seq_, myrec_,
+                             piv_dev_, &piv_host_[par], S_SIDE);
+    prof_end(PH_PIVOT, pe, S_SIDE);
+  } else {
+    dev_.pivot_local(scores_, valid_, used_, pos_, L_, myrec_, S_SIDE);
+    prof_end(PH_PIVOT, pe, S_SIDE);
+    pe = prof_begin(S_SIDE);
+    comm_.allgather(dev_, myrec_, recs_, sizeof(PivotRec), S_SIDE);
+    piv_host_[par].step = -1;
+    dev_.pivot_global(recs_, (int32_t)L_.p, (int32_t)t, pos_, phys_at_, used_, seq_, piv_dev_,
+                      &piv_host_[par], S_SIDE);
+    prof_end(PH_EXCHANGE, pe, S_SIDE);
+  }
   dev_.record(ev_sel_[par], S_SIDE);
   dbg_sync();
 }
