@@ -166,6 +166,7 @@ class Engine {
   Layout L_;
   int d_ = 1;
   std::string bcast_algo_ = "ring";
+  bool comm_small_tiles_ = false;  // COMM chunk-normalisation GEMMs on the small latency tile
   double norm_a_ = -1;
 
   // chunk plan (block-column ranges, multiples of d_ blocks so a panel never straddles chunks)

@@ -78,6 +78,12 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // p=8 emulation 0.191 vs 0.166 s (two concurrent GEMMs interleave their tiles, lose L2 locality
   // and crowd out the pivot path) — so off by default.
   if (const char* e = std::getenv("GJ_TWO_MAIN_STREAMS")) two_main_ = std::atoi(e) != 0;
+  // COMM chunk-normalisation GEMMs (m x chunk width x m) on the small 64x32 latency tile: 4x the
+  // workgroups of the 128x64 tile.  Measured (profiles/small_n_sweep.md): N = 8192 30.2 -> 29.3 ms,
+  // but N = 16384 +1.1 % and N = 32768 +0.7 % (more COMM workgroups beside the trailing update), so
+  // only where the pivot chain dominates (padded order <= 8192).  GJ_COMM_SMALL_TILES overrides.
+  comm_small_tiles_ = L_.npad <= 8192;
+  if (const char* e = std::getenv("GJ_COMM_SMALL_TILES")) comm_small_tiles_ = std::atoi(e) != 0;
   two_main_ = two_main_ && cb0_.size() > 1;
 
   // CU reservation for the latency-bound panel factorisation (GJ_RESERVE_CUS overrides).
@@ -496,17 +502,19 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
       int pe = prof_begin(S_COMM);
       if (r.owner == L_.k) {
         const int64_t sl = r.phys / L_.p;
+        GemmExtra lat;
+        lat.latency = comm_small_tiles_;
         for (int64_t z = 0; z < nr; ++z) {
           const int64_t a = ra[z], w = rb[z] - ra[z];
           if (j == 0) {
             dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, w, m, Ht_[par][j], m,
-                      elem(X_, sl * m * npad + a), npad, seg + (a - c0) * (int64_t)es, W, S_COMM);
+                      elem(X_, sl * m * npad + a), npad, seg + (a - c0) * (int64_t)es, W, S_COMM, lat);
           } else {
             dev_.copy2d(T_, W * es, elem(X_, sl * m * npad + a), npad * es, w * es, m, S_COMM);
             dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, m, w, j * m, Lrow_[par][j], m,
-                      chunk + (a - c0) * (int64_t)es, W, T_, W, S_COMM);
+                      chunk + (a - c0) * (int64_t)es, W, T_, W, S_COMM, lat);
             dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, w, m, Ht_[par][j], m, T_, W,
-                      seg + (a - c0) * (int64_t)es, W, S_COMM);
+                      seg + (a - c0) * (int64_t)es, W, S_COMM, lat);
           }
         }
         if (has_panel) {  // panel columns: PP_t for blocks <= t, zero for later panel blocks
