@@ -19,7 +19,7 @@ HIPFLAGS  := $(COMMON) --offload-arch=$(ARCH) -mcode-object-version=5 -munsafe-f
 HOSTFLAGS := $(COMMON) -x c++ -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
 LDLIBS    := -L$(ROCM)/lib -lrccl -lamdhip64 -lrocprofiler-sdk-roctx -lpthread
 
-KERNELS   := gemm gemm_valu blockinv misc
+KERNELS   := gemm gemm_valu blockinv blockinv_mfma misc
 HOST_SRC  := solver/engine solver/runner runtime/host_device runtime/hip_device \
              runtime/loopback_comm runtime/shadow_comm runtime/rccl_comm runtime/comm io/matrix_io
 
@@ -31,7 +31,7 @@ PYEXT     := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_config_v
 PYINC     := $(shell $(PYTHON) -c "import sysconfig,pybind11;print('-I'+sysconfig.get_paths()['include'],'-I'+pybind11.get_include())")
 PYMOD     := $(PKG)/_C$(PYEXT)
 
-HEADERS   := $(wildcard csrc/include/gj/*.hpp) csrc/kernels/kernels.hpp
+HEADERS   := $(wildcard csrc/include/gj/*.hpp) $(wildcard csrc/kernels/*.hpp)
 
 # Host-code sanitizer build: the host runtime, engine, communicators and I/O
 # under ASan + UBSan; device code is not instrumented (GPU sanitizers are not available here).

@@ -1,12 +1,11 @@
 #!/usr/bin/env python3
-"""Latency of the batched candidate-block inversion (pivot search) in isolation.
+"""Latency of the batched candidate-block inversion (pivot search) in isolation (device-side events).
 
-    python bench/bench_blockinv.py [panel] [sweep]
+    python bench/bench_blockinv.py [panel] [panel_rl] [panel1] [sweep]
 """
 import json
 import os
 import sys
-import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
@@ -23,14 +22,13 @@ def main(variants):
                 for dt in (torch.float64, torch.float32):
                     Lt = torch.randn(m, nblk * m, dtype=dt, device="cuda")
                     n = nblk * m
-                    ops.block_inverse(Lt, n, m)
+                    inv_t, scores, valid = ops.block_inverse(Lt, n, m)
+                    used = torch.zeros(nblk, dtype=torch.int32, device="cuda")
                     torch.cuda.synchronize()
-                    reps = 20
-                    t0 = time.perf_counter()
-                    for _ in range(reps):
-                        ops.block_inverse(Lt, n, m)
-                    torch.cuda.synchronize()
-                    us = (time.perf_counter() - t0) / reps * 1e6
+                    # device-side: 50 back-to-back launches between two events
+                    us = ops.device_for(Lt).time_block_inverse(
+                        ops._DT[dt], Lt.data_ptr(), Lt.stride(0), inv_t.data_ptr(), scores.data_ptr(),
+                        valid.data_ptr(), used.data_ptr(), n, m, 1, 0, 0.0, 50)
                     print(json.dumps({"variant": var, "m": m, "nblk": nblk, "dtype": str(dt).split(".")[-1],
                                       "us_per_call": round(us, 1), "us_per_step": round(us / m, 3)}), flush=True)
     C.set_block_inverse_variant("panel")

@@ -20,41 +20,11 @@
 #include <cstdint>
 
 #include "kernels.hpp"
+#include "wave_ops.hpp"
 
 namespace gj {
 namespace kern {
 
-// ---- wave-wide max of a double without LDS round trips: DPP quad/row permutes for the first
-// 16 lanes, v_permlane16_swap / v_permlane32_swap (gfx950) for the rest.
-template <int CTRL>
-__device__ __forceinline__ double dpp64(double x) {
-  const uint64_t b = __builtin_bit_cast(uint64_t, x);
-  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)b, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, false);
-  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-}
-__device__ __forceinline__ double join64(unsigned lo, unsigned hi) {
-  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-}
-__device__ __forceinline__ double wave_max_f64(double v) {
-  v = fmax(v, dpp64<0xB1>(v));   // quad_perm [1,0,3,2]
-  v = fmax(v, dpp64<0x4E>(v));   // quad_perm [2,3,0,1]
-  v = fmax(v, dpp64<0x141>(v));  // row_half_mirror (8)
-  v = fmax(v, dpp64<0x140>(v));  // row_mirror (16)
-  {
-    const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    const auto l = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
-    const auto h = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
-    v = fmax(join64(l[0], h[0]), join64(l[1], h[1]));
-  }
-  {
-    const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    const auto l = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
-    const auto h = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
-    v = fmax(join64(l[0], h[0]), join64(l[1], h[1]));
-  }
-  return v;
-}
 // Same for non-negative keys compared as integers (no NaN canonicalisation on the chain).
 __device__ __forceinline__ uint64_t umax64(uint64_t a, uint64_t b) { return a > b ? a : b; }
 template <int CTRL>
@@ -283,18 +253,6 @@ __global__ __launch_bounds__(NTH) void block_inverse_kernel(const T* __restrict_
 //            permlane wave max, pivot row by v_readlane (no LDS, no barrier inside a step);
 //   phase B  (all waves): rank-16 update of the other columns from U and the 16 pivot rows (LDS).
 // 3 workgroup barriers per panel instead of 2 per step.
-template <typename T>
-__device__ __forceinline__ T readlane_t(T v, int lane) {
-  if constexpr (sizeof(T) == 8) {
-    const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, lane);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), lane);
-    return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
-  } else {
-    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
-  }
-}
-
 #ifdef GJ_BI_PROBE  // phase timestamps of workgroup 0 (bench/blockinv_probe.hip)
 __device__ unsigned long long g_bi_probe[256];
 #define BI_PROBE(slot)                                                            \
@@ -692,7 +650,7 @@ __global__ __launch_bounds__(256) void block_inverse_generic(const T* __restrict
   }
 }
 
-static int g_bi_variant = 0;  // 0 = panel-blocked (default), 1 = per-step sweep
+static int g_bi_variant = 0;  // 0 = matrix-core panels (default), 1 = per-step sweep, 2 = one-wave panels
 void set_block_inverse_variant(int v) { g_bi_variant = v; }
 int block_inverse_variant() { return g_bi_variant; }
 
@@ -704,10 +662,14 @@ static void launch_bi(const void* Lt, int64_t ldl, void* inv_t, double* scores, 
   const unsigned grid = (unsigned)L.nblk;
   const T* lt = static_cast<const T*>(Lt);
   T* it = static_cast<T*>(inv_t);
-  if (g_bi_variant == 0 && m > 32 && m <= 64)
+  if ((g_bi_variant == 0 || g_bi_variant == 3) &&
+      block_inverse_mfma(sizeof(T) == 8 ? DType::F64 : DType::F32, Lt, ldl, inv_t, scores, valid, used,
+                         L, thresh, s, g_bi_variant == 0))
+    return;
+  if (g_bi_variant == 2 && m > 32 && m <= 64)
     hipLaunchKernelGGL((block_inverse_panel_kernel<T, 64, 256>), dim3(grid), dim3(256), 0, s, lt, ldl,
                        it, scores, valid, used, m, L.p, L.k, thresh);
-  else if (g_bi_variant == 0 && m > 64 && m <= 128)
+  else if (g_bi_variant == 2 && m > 64 && m <= 128)
     hipLaunchKernelGGL((block_inverse_panel_kernel<T, 128, 512>), dim3(grid), dim3(512), 0, s, lt, ldl,
                        it, scores, valid, used, m, L.p, L.k, thresh);
   else if (m <= 32)

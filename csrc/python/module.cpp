@@ -134,7 +134,9 @@ PYBIND11_MODULE(_C, mod) {
   mod.def("set_block_inverse_variant", [](const std::string& v) {
     if (v == "panel") kern::set_block_inverse_variant(0);
     else if (v == "sweep") kern::set_block_inverse_variant(1);
-    else throw std::invalid_argument("block inverse variant: panel | sweep");
+    else if (v == "panel1") kern::set_block_inverse_variant(2);
+    else if (v == "panel_lds") kern::set_block_inverse_variant(3);
+    else throw std::invalid_argument("block inverse variant: panel | sweep | panel1 | panel_lds");
   });
   mod.def("set_gemm_variant", [](const std::string& v) { kern::set_gemm_variant(kern::gemm_variant_id(v.c_str())); });
 
@@ -205,6 +207,25 @@ PYBIND11_MODULE(_C, mod) {
              d.block_inverse(parse_dtype(dt), (const void*)Lt, ldl, (void*)inv_t, (double*)scores,
                              (int32_t*)valid, (const int32_t*)used, lay(n, m, p, k), thresh, S_MAIN);
              d.sync_stream(S_MAIN);
+           })
+      // Device-side latency of the batched block inverse: `reps` back-to-back launches on one
+      // stream between two timing events (no host work in between); returns microseconds per call.
+      .def("time_block_inverse",
+           [lay](Device& d, const std::string& dt, U Lt, int64_t ldl, U inv_t, U scores, U valid,
+                 U used, int64_t n, int64_t m, int64_t p, int64_t k, double thresh, int reps) {
+             py::gil_scoped_release rel;
+             const Layout L = lay(n, m, p, k);
+             const DType t = parse_dtype(dt);
+             d.block_inverse(t, (const void*)Lt, ldl, (void*)inv_t, (double*)scores, (int32_t*)valid,
+                             (const int32_t*)used, L, thresh, S_SIDE);
+             const int e0 = d.create_event(true), e1 = d.create_event(true);
+             d.record(e0, S_SIDE);
+             for (int i = 0; i < reps; ++i)
+               d.block_inverse(t, (const void*)Lt, ldl, (void*)inv_t, (double*)scores, (int32_t*)valid,
+                               (const int32_t*)used, L, thresh, S_SIDE);
+             d.record(e1, S_SIDE);
+             d.sync_stream(S_SIDE);
+             return 1e3 * d.event_ms(e0, e1) / std::max(reps, 1);
            })
       .def("permute_blocks",
            [](Device& d, const std::string& dt, U dst, int64_t ldd, U X, int64_t ldx, int64_t nblk,
