@@ -7,7 +7,7 @@
 #include <random>
 #include <vector>
 
-template <int MP, bool RL>
+template <int MP, int RL>
 static void run(int m, int nblk) {
   using namespace gj::kern;
   std::vector<double> h((size_t)m * nblk * m);
@@ -40,12 +40,13 @@ static void run(int m, int nblk) {
     if (rep < 2) continue;
     const double t0 = (double)pr[1002];
     std::printf("%s m=%d nblk=%d: kernel %.1f us (event); shader cycles from wave-0 start:\n",
-                RL ? "readlane-bcast" : "lds-bcast", m, nblk, ms * 1e3);
+                RL == 2 ? "pipelined" : RL == 1 ? "readlane-bcast" : "lds-bcast", m, nblk, ms * 1e3);
     std::printf("  load done %.0f | pivot wave at B0(0) %.0f\n", pr[512] - t0, pr[0] - t0);
-    double steps = 0;
+    double steps = 0, aph = 0;
     int nst = 0;
     for (int q = 0; q < m / 16; ++q) {
       const unsigned long long* P = pr + 8 + 24 * q;
+      aph += (double)(P[17] - P[0]);
       std::printf("  panel %d: A start %.0f, 16 steps %.0f (", q, P[0] - t0, (double)(P[16] - P[0]));
       for (int j = 0; j < 16; ++j) {
         const double d = (double)(P[1 + j] - (j ? P[j] : P[0]));
@@ -59,15 +60,16 @@ static void run(int m, int nblk) {
                   (double)(B[1] - B[0]), (double)(B[2] - B[1]), (double)(B[3] - B[2]),
                   (double)(B[4] - B[3]), q + 1 < m / 16 ? (double)(B[8] - B[4]) : 0.0);
     }
+    std::printf("  A phase (steps + publish) per step %.0f cycles\n", aph / (16.0 * (m / 16)));
     std::printf("  mean step %.0f cycles; epilogue (staged output + norm) %.0f; end %.0f\n", steps / nst,
                 (double)(pr[1001] - pr[1000]), pr[1001] - t0);
   }
 }
 
 int main() {
-  run<128, false>(128, 32);
-  run<128, true>(128, 32);
-  run<64, false>(64, 32);
-  run<64, true>(64, 32);
+  run<128, 1>(128, 32);
+  run<128, 2>(128, 32);
+  run<64, 1>(64, 32);
+  run<64, 2>(64, 32);
   return 0;
 }

@@ -10,6 +10,7 @@
 // Every op takes a stream role (S_MAIN/S_SIDE/S_COMM); the host device executes synchronously.
 #pragma once
 
+#include <memory>
 #include <string>
 
 #include "gj/common.hpp"
@@ -89,6 +90,17 @@ class Device {
   virtual void sync_all() = 0;
   virtual float event_ms(int ev_start, int ev_end) = 0;
   virtual void* native_stream(int s) = 0;  // hipStream_t (nullptr on host)
+  // Cross-device ordering points (the asynchronous virtual-rank transport, AsyncLoopbackComm):
+  // mark(s) enqueues a marker on stream s and returns a handle that completes when everything
+  // enqueued on s before it has; wait_mark(s, h) makes stream s wait for a handle from ANY device
+  // of the same kind in this process (HIP: an event, so the same GPU or peer GPUs; host: a fence).
+  // A null handle means "already complete".  Devices that execute synchronously return null.
+  virtual std::shared_ptr<void> mark(int s) { (void)s; return nullptr; }
+  virtual void wait_mark(int s, const std::shared_ptr<void>& h) { (void)s; (void)h; }
+  // Timing / scheduling probes: keep stream s busy for `us` microseconds on `nwg` workgroups
+  // (nwg = 1: a pure delay, e.g. per-rank start jitter; more: the CU footprint of a transfer in the
+  // single-GPU communication-cost model of ShadowComm).  No-op where it has no meaning.
+  virtual void occupy(int s, int nwg, double us) { (void)s; (void)nwg; (void)us; }
   // Keep the MAIN (trailing-update) stream off `n` CUs so the latency-critical SIDE/COMM kernels
   // always find idle CUs (mode 0: CUs 0..n-1 of the mask, mode 1: spread over the mask).
   // Returns the number of CUs actually reserved.  Call while the device is idle.

@@ -662,9 +662,9 @@ static void launch_bi(const void* Lt, int64_t ldl, void* inv_t, double* scores, 
   const unsigned grid = (unsigned)L.nblk;
   const T* lt = static_cast<const T*>(Lt);
   T* it = static_cast<T*>(inv_t);
-  if ((g_bi_variant == 0 || g_bi_variant == 3) &&
+  if ((g_bi_variant == 0 || g_bi_variant == 3 || g_bi_variant == 4) &&
       block_inverse_mfma(sizeof(T) == 8 ? DType::F64 : DType::F32, Lt, ldl, inv_t, scores, valid, used,
-                         L, thresh, s, g_bi_variant == 0))
+                         L, thresh, s, g_bi_variant == 0 ? 2 : g_bi_variant == 4 ? 1 : 0))
     return;
   if (g_bi_variant == 2 && m > 32 && m <= 64)
     hipLaunchKernelGGL((block_inverse_panel_kernel<T, 64, 256>), dim3(grid), dim3(256), 0, s, lt, ldl,

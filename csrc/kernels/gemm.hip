@@ -666,7 +666,8 @@ static void launch(const GemmArgs& a, hipStream_t s) {
     // kernel (61 TF/s vs 57.6 register-staged at 32768x4096x512), fp32 the 64x64-per-wave square
     // tile (110.5 TF/s).  Everything else keeps the register-staged narrow tile.
     const int64_t big_tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
-    const bool deep = a.K >= 384 && big_tiles >= 512;
+    static const int64_t min_k = getenv("GJ_GLDS_MINK") ? atoll(getenv("GJ_GLDS_MINK")) : 384;
+    const bool deep = a.K >= min_k && big_tiles >= 512;
     v = !deep ? 1 : (sizeof(T) == 8 ? 11 : 6);
   }
   if (v == 11) {  // LDS-DMA fp64 kernel; other dtypes / layouts / alignments take the next best tile

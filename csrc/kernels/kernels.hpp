@@ -23,7 +23,7 @@ void gemm_valu(int op, int64_t M, int64_t N, int64_t K, const void* At, int64_t 
                int64_t ldb, void* C, int64_t ldc, hipStream_t s, const GemmExtra* ex);
 int gemm_variant_id(const char* name);  // big | narrow | tall | valu
 void set_gemm_variant(int v);
-void set_block_inverse_variant(int v);  // 0/3 = matrix-core panels (readlane / LDS row bcast), 1 = sweep, 2 = one-wave panels
+void set_block_inverse_variant(int v);  // 0/3/4 = matrix-core panels (pipelined / LDS / readlane row bcast), 1 = sweep, 2 = one-wave panels
 int block_inverse_variant();
 void residual_partial(DType dt, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                       const void* B, int64_t ldb, int64_t n_real, int64_t blk_m, int64_t p,
@@ -36,7 +36,7 @@ void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* s
 // blockinv_mfma.hip: 16 < m <= 128 (false = not handled)
 bool block_inverse_mfma(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                         int32_t* valid, const int32_t* used, const Layout& L, double thresh,
-                        hipStream_t s, bool readlane_bcast);
+                        hipStream_t s, int pivot_variant /*0 LDS, 1 readlane, 2 pipelined*/);
 // scratch needed by the generic (m > 256) path
 size_t block_inverse_scratch_bytes(DType dt, const Layout& L);
 size_t block_inverse_iscratch_bytes(const Layout& L);

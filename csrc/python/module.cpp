@@ -136,7 +136,8 @@ PYBIND11_MODULE(_C, mod) {
     else if (v == "sweep") kern::set_block_inverse_variant(1);
     else if (v == "panel1") kern::set_block_inverse_variant(2);
     else if (v == "panel_lds") kern::set_block_inverse_variant(3);
-    else throw std::invalid_argument("block inverse variant: panel | sweep | panel1 | panel_lds");
+    else if (v == "panel_rl") kern::set_block_inverse_variant(4);
+    else throw std::invalid_argument("block inverse variant: panel | sweep | panel1 | panel_lds | panel_rl");
   });
   mod.def("set_gemm_variant", [](const std::string& v) { kern::set_gemm_variant(kern::gemm_variant_id(v.c_str())); });
 
