@@ -21,7 +21,8 @@ LDLIBS    := -L$(ROCM)/lib -lrccl -lamdhip64 -lrocprofiler-sdk-roctx -lpthread
 
 KERNELS   := gemm gemm_valu blockinv blockinv_mfma misc
 HOST_SRC  := solver/engine solver/runner runtime/host_device runtime/hip_device \
-             runtime/loopback_comm runtime/shadow_comm runtime/rccl_comm runtime/comm io/matrix_io
+             runtime/loopback_comm runtime/async_loopback_comm runtime/async_host_device \
+             runtime/shadow_comm runtime/rccl_comm runtime/comm io/matrix_io
 
 KOBJ      := $(patsubst %,$(BUILD)/kernels/%.o,$(KERNELS))
 HOBJ      := $(patsubst %,$(BUILD)/%.o,$(HOST_SRC))

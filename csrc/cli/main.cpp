@@ -13,7 +13,7 @@
 //   -p, --ranks P        number of ranks (GPUs with --device gpu, virtual ranks with --device cpu)
 //   --gpus P             alias of --ranks for GPU runs
 //   --device gpu|cpu     execution backend (default: gpu when a HIP device exists)
-//   --comm auto|rccl|loopback
+//   --comm auto|rccl|loopback|async   (async: stream-ordered virtual ranks; --jitter US)
 //   --dtype fp64|fp32
 //   --gen absdiff|hilbert|random|identity   generator when no file is given (reference: absdiff;
 //                        -DHILBERT -> --gen hilbert)
@@ -103,6 +103,7 @@ int main(int argc, char* argv[]) {
       if (a == "-p" || a == "--ranks" || a == "--gpus") cfg.ranks = std::atoi(val(a.c_str()));
       else if (a == "--device") device = val("--device");
       else if (a == "--comm") cfg.comm = val("--comm");
+      else if (a == "--jitter") cfg.jitter_us = std::atof(val("--jitter"));
       else if (a == "--dtype") {
         const std::string d = val("--dtype");
         if (d == "fp64" || d == "f64" || d == "double") cfg.solve.dtype = DType::F64;

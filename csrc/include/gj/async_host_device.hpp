@@ -1,26 +1,42 @@
-// HipDevice — the MI355X execution backend (csrc/runtime/hip_device.cpp).
+// AsyncHostDevice — the host executor with REAL asynchronous streams (csrc/runtime/async_host_device.cpp).
+//
+// HostDevice runs every op before it returns, so a missing event dependency between the engine's
+// MAIN / SIDE / COMM streams can never show on the CPU.  Here every stream role is a worker thread
+// with an in-order queue (the ops run HostDevice's code), events are fences recorded into those
+// queues, and `jitter_us` inserts random delays before queued ops so that the streams interleave
+// differently on every run — the same hazards a GPU has, testable without one.
 #pragma once
 
+#include <condition_variable>
+#include <deque>
+#include <exception>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <random>
+#include <thread>
 #include <vector>
 
-#include "gj/device.hpp"
+#include "gj/host_device.hpp"
 
 namespace gj {
 
-class HipDevice : public Device {
+class AsyncHostDevice : public Device {
  public:
-  explicit HipDevice(int device_index);
-  ~HipDevice() override;
-  bool on_gpu() const override { return true; }
+  // nthreads: threads of each op (HostDevice); jitter_us > 0: a random delay in [0, jitter_us)
+  // before about one op in four on every stream; wait_timeout_s: a stream waiting longer than this
+  // for an event fails (reported at the next synchronisation) instead of hanging.
+  explicit AsyncHostDevice(int nthreads = 1, double jitter_us = 0.0, uint64_t seed = 0,
+                           double wait_timeout_s = 120.0);
+  ~AsyncHostDevice() override;
+  bool on_gpu() const override { return false; }
   std::string describe() const override;
-  int device_index() const override { return dev_; }
 
-  void* alloc(size_t bytes) override;
+  void* alloc(size_t bytes) override { return inner_.alloc(bytes); }
   void release(void* p) override;
-  void* alloc_pinned(size_t bytes) override;
-  void* alloc_pinned_coherent(size_t bytes) override;
+  void* alloc_pinned(size_t bytes) override { return inner_.alloc_pinned(bytes); }
   void release_pinned(void* p) override;
-  size_t free_memory() const override;
+  size_t free_memory() const override { return inner_.free_memory(); }
   void memset0(void* p, size_t bytes, int s) override;
   void memset2d(void* p, size_t pitch, size_t width_bytes, size_t height, int s) override;
   void copy(void* dst, const void* src, size_t bytes, int s) override;
@@ -32,15 +48,10 @@ class HipDevice : public Device {
   void wait(int s, int ev) override;
   void sync_event(int ev) override;
   bool query_event(int ev) override;
- private:
-  int reserved_ = 0, reserve_mode_ = 0;
-
- public:
-  int reserve_cus(int n, int mode) override;
   void sync_stream(int s) override;
   void sync_all() override;
   float event_ms(int ev_start, int ev_end) override;
-  void* native_stream(int s) override;
+  void* native_stream(int) override { return nullptr; }
   std::shared_ptr<void> mark(int s) override;
   void wait_mark(int s, const std::shared_ptr<void>& h) override;
   void occupy(int s, int nwg, double us) override;
@@ -56,9 +67,6 @@ class HipDevice : public Device {
                      int s) override;
   void pivot_local(const double* scores, const int32_t* valid, const int32_t* used,
                    const int32_t* pos, const Layout& L, PivotRec* out, int s) override;
-  void pivot_select_single(const double* scores, const int32_t* valid, const Layout& L, int32_t t,
-                           int32_t* pos, int32_t* phys_at, int32_t* used, int32_t* seq, PivotRec* rec,
-                           PivotResult* out, PivotResult* host_out, int s) override;
   void pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos, int32_t* phys_at,
                     int32_t* used, int32_t* seq, PivotResult* out, PivotResult* host_out,
                     int s) override;
@@ -68,7 +76,6 @@ class HipDevice : public Device {
   void gemm(DType dt, GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const void* A,
             int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int s,
             const GemmExtra& ex = GemmExtra()) override;
-  void gemm_batch(DType dt, const GemmDesc* d, int n, int s) override;
   void permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx, int64_t nblk,
                       int64_t m, int64_t Nr, const int32_t* dst_blk, const int32_t* colsrc,
                       int s) override;
@@ -77,15 +84,39 @@ class HipDevice : public Device {
   void residual(DType dt, const void* A, const void* Full, const Layout& L, double* out,
                 int s) override;
 
- private:
-  void* scratch(size_t bytes, int slot);
-  void activate() const;
+  // A fence between queues: signalled by the stream that records it, waited on by any stream
+  // (of any AsyncHostDevice of this process) or by the host.
+  struct Fence {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false;
+    double t_ms = 0.0;
+    void signal();
+    bool wait_for(double seconds);
+  };
 
-  int dev_ = 0;
-  void* streams_[kNumStreams] = {};
-  std::vector<void*> events_;
-  void* scratch_[2] = {nullptr, nullptr};
-  size_t scratch_sz_[2] = {0, 0};
+ private:
+  struct Worker {
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::function<void()>> q;
+    bool stop = false;
+    std::mt19937_64 rng;
+  };
+  void enqueue(int s, std::function<void()> f);
+  void run(int s);
+  void fail(std::exception_ptr e);
+  void rethrow();
+  void check_stream(int s) const;
+
+  HostDevice inner_;
+  double jitter_us_, wait_timeout_s_;
+  Worker w_[kNumStreams];
+  std::mutex ev_mu_;
+  std::vector<std::shared_ptr<Fence>> ev_last_;  // per event: the fence of its latest record
+  std::mutex err_mu_;
+  std::exception_ptr err_;
 };
 
 }  // namespace gj

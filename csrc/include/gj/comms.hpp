@@ -58,19 +58,28 @@ class LoopbackHub {
  public:
   explicit LoopbackHub(int p);
   int size() const { return p_; }
+  // Rendezvous of all ranks; throws Error(CommError) once any rank has called fail() (a rank that
+  // died must not leave its peers blocked forever).
   void arrive_and_wait();
+  void fail(const std::string& why);
+  bool failed() const;
   // published pointers / values
   std::vector<const void*> ptr;
   std::vector<double> val;
   std::vector<std::vector<P2POp>> p2p;  // per source rank
   std::vector<std::string> sig;          // per rank: signature of the collective being entered
+  // AsyncLoopbackComm: per rank, the marker at which its stream reached the collective and the
+  // marker after its own copies (Device::mark handles)
+  std::vector<std::shared_ptr<void>> mk, done;
 
  private:
   int p_;
-  std::mutex mu_;
+  mutable std::mutex mu_;
   std::condition_variable cv_;
   int count_ = 0;
   long gen_ = 0;
+  bool failed_ = false;
+  std::string why_;
 };
 
 class LoopbackComm : public Comm {
@@ -95,6 +104,45 @@ class LoopbackComm : public Comm {
   void enter(const std::string& signature);
   std::shared_ptr<LoopbackHub> hub_;
   int r_;
+};
+
+// ---------------------------------------------------------------- asynchronous virtual ranks
+// p ranks as threads of one process (one GPU, several GPUs, or AsyncHostDevice on the CPU) whose
+// collectives are STREAM-ORDERED, like RCCL's: no stream is ever drained.  A collective records a
+// marker on the issuing stream (Device::mark); after a host rendezvous that exchanges buffer
+// pointers and markers, every rank's stream waits on its peers' markers (Device::wait_mark) and
+// copies on its own stream, then the owners of read buffers wait for the readers' "done" markers
+// before their stream may overwrite them.  The host threads only meet to swap pointers, so COMM
+// broadcasts really race MAIN GEMMs through events, as on 8 GPUs.  jitter_us > 0 delays each
+// rank's arrival at random (a device-side delay on the stream and a host-side one), so the ranks
+// reach every collective in a different order on every run.
+class AsyncLoopbackComm : public Comm {
+ public:
+  AsyncLoopbackComm(std::shared_ptr<LoopbackHub> hub, int rank, double jitter_us = 0.0,
+                    uint64_t seed = 0);
+  int size() const override { return hub_->size(); }
+  int rank() const override { return r_; }
+  std::string describe() const override;
+
+  void allgather(Device& dev, const void* send, void* recv, size_t bytes, int s) override;
+  void bcast(Device& dev, void* buf, size_t bytes, int root, int s) override;
+  void allreduce_max(Device& dev, double* buf, size_t count, int s) override;
+  void group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) override;
+  void barrier(Device& dev) override;
+  double host_max(Device& dev, double v) override;
+  void host_allgather(Device& dev, const void* send, void* recv, size_t bytes) override;
+  void check_health() override;
+  void abort() override;
+
+ private:
+  void jitter(Device& dev, int s);
+  // publish (signature, pointer, marker[, sends]) and meet; throws on an SPMD mismatch
+  void enter(const std::string& signature, const void* p, std::shared_ptr<void> mk,
+             const std::vector<P2POp>* sends = nullptr);
+  std::shared_ptr<LoopbackHub> hub_;
+  int r_;
+  double jitter_us_;
+  uint64_t rng_;
 };
 
 }  // namespace gj

@@ -16,7 +16,8 @@ struct RunConfig {
   int64_t n = 0, m = 0;
   int ranks = 1;
   bool gpu = true;
-  std::string comm = "auto";        // auto | rccl | loopback
+  std::string comm = "auto";        // auto | rccl | loopback | async (stream-ordered virtual ranks)
+  double jitter_us = 0.0;           // async: random per-rank arrival delay (tests)
   int first_device = 0;
   GenSpec gen;
   std::string file;                 // input file (text or .bin); empty => generator

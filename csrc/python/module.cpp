@@ -430,6 +430,7 @@ PYBIND11_MODULE(_C, mod) {
     if (d.contains("ranks")) c.ranks = d["ranks"].cast<int>();
     if (d.contains("device")) c.gpu = d["device"].cast<std::string>() == "gpu";
     if (d.contains("comm")) c.comm = d["comm"].cast<std::string>();
+    if (d.contains("jitter_us")) c.jitter_us = d["jitter_us"].cast<double>();
     if (d.contains("gen")) c.gen.kind = parse_gen(d["gen"].cast<std::string>());
     if (d.contains("seed")) c.gen.seed = d["seed"].cast<uint64_t>();
     if (d.contains("file")) c.file = d["file"].cast<std::string>();

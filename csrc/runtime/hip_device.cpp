@@ -165,6 +165,22 @@ float HipDevice::event_ms(int a, int b) {
   return ms;
 }
 void* HipDevice::native_stream(int s) { return streams_[s]; }
+static void check_launch();
+// A marker is an event of its own (recorded once): other devices' streams wait on it by handle.
+std::shared_ptr<void> HipDevice::mark(int s) {
+  activate();
+  hipEvent_t e;
+  HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HIP_OK(hipEventRecord(e, hs(streams_[s])));
+  return std::shared_ptr<void>(static_cast<void*>(e), [](void* p) { (void)hipEventDestroy(static_cast<hipEvent_t>(p)); });
+}
+void HipDevice::wait_mark(int s, const std::shared_ptr<void>& h) {
+  if (h) HIP_OK(hipStreamWaitEvent(hs(streams_[s]), static_cast<hipEvent_t>(h.get()), 0));
+}
+void HipDevice::occupy(int s, int nwg, double us) {
+  kern::spin(nwg, us, hs(streams_[s]));
+  check_launch();
+}
 
 void* HipDevice::scratch(size_t bytes, int slot) {
   if (bytes > scratch_sz_[slot]) {

@@ -8,18 +8,34 @@
 
 namespace gj {
 
-LoopbackHub::LoopbackHub(int p) : ptr(p, nullptr), val(p, 0.0), p2p(p), sig(p), p_(p) {}
+LoopbackHub::LoopbackHub(int p) : ptr(p, nullptr), val(p, 0.0), p2p(p), sig(p), mk(p), done(p), p_(p) {}
 
 void LoopbackHub::arrive_and_wait() {
   std::unique_lock<std::mutex> lk(mu_);
+  if (failed_) throw Error(Status::CommError, "peer rank failed: " + why_);
   const long g = gen_;
   if (++count_ == p_) {
     count_ = 0;
     ++gen_;
     cv_.notify_all();
   } else {
-    cv_.wait(lk, [&] { return gen_ != g; });
+    cv_.wait(lk, [&] { return gen_ != g || failed_; });
+    if (gen_ == g) throw Error(Status::CommError, "peer rank failed: " + why_);
   }
+}
+
+void LoopbackHub::fail(const std::string& why) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!failed_) {
+    failed_ = true;
+    why_ = why;
+  }
+  cv_.notify_all();
+}
+
+bool LoopbackHub::failed() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return failed_;
 }
 
 void LoopbackComm::enter(const std::string& signature) {

@@ -10,6 +10,7 @@
 #include <mutex>
 #include <thread>
 
+#include "gj/async_host_device.hpp"
 #include "gj/comms.hpp"
 #include "gj/gen.hpp"
 #include "gj/hip_device.hpp"
@@ -33,6 +34,7 @@ void rank_main(const RunConfig& cfg, int rank, Shared& sh, std::shared_ptr<Loopb
                const std::vector<std::string>& ids, bool use_rccl) {
   std::unique_ptr<Device> dev;
   std::unique_ptr<Comm> comm;
+  const bool async = cfg.comm == "async";
   if (cfg.gpu) {
     int ndev = 0;
     (void)hipGetDeviceCount(&ndev);
@@ -43,14 +45,22 @@ void rank_main(const RunConfig& cfg, int rank, Shared& sh, std::shared_ptr<Loopb
       comm.reset(new RcclComm(ids, cfg.ranks, rank, d));
     else if (cfg.ranks == 1)
       comm.reset(new SelfComm());
+    else if (async)
+      comm.reset(new AsyncLoopbackComm(hub, rank, cfg.jitter_us, cfg.gen.seed));
     else
       comm.reset(new LoopbackComm(hub, rank));
   } else {
     const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
     const int nt = cfg.host_threads > 0 ? cfg.host_threads : std::max(1, hw / cfg.ranks);
-    dev.reset(new HostDevice(nt));
+    if (async)  // real asynchronous streams on the CPU (one worker thread per stream role)
+      dev.reset(new AsyncHostDevice(nt, cfg.jitter_us, cfg.gen.seed * 131u + (uint64_t)rank,
+                                    cfg.solve.comm_timeout_s));
+    else
+      dev.reset(new HostDevice(nt));
     if (cfg.ranks == 1)
       comm.reset(new SelfComm());
+    else if (async)
+      comm.reset(new AsyncLoopbackComm(hub, rank, cfg.jitter_us, cfg.gen.seed));
     else
       comm.reset(new LoopbackComm(hub, rank));
   }
@@ -242,12 +252,32 @@ RunReport run_local(const RunConfig& cfg) {
     ids.push_back(RcclComm::unique_id());
   }
   auto hub = std::make_shared<LoopbackHub>(cfg.ranks);
+  // A rank that throws (a transport error, a timed-out wait, a failed launch) reports it and
+  // poisons the hub, so its peers leave their next rendezvous with an error instead of hanging.
+  auto guarded = [&](int r) {
+    try {
+      rank_main(cfg, r, sh, hub, ids, use_rccl);
+    } catch (const Error& e) {
+      hub->fail(e.what());
+      std::lock_guard<std::mutex> lk(sh.mu);
+      if (sh.rep.status == Status::Ok) {
+        sh.rep.status = e.status();
+        sh.rep.message = e.what();
+      }
+    } catch (const std::exception& e) {
+      hub->fail(e.what());
+      std::lock_guard<std::mutex> lk(sh.mu);
+      if (sh.rep.status == Status::Ok) {
+        sh.rep.status = Status::CommError;
+        sh.rep.message = e.what();
+      }
+    }
+  };
   if (cfg.ranks == 1) {
-    rank_main(cfg, 0, sh, hub, ids, use_rccl);
+    guarded(0);
   } else {
     std::vector<std::thread> th;
-    for (int r = 0; r < cfg.ranks; ++r)
-      th.emplace_back([&, r] { rank_main(cfg, r, sh, hub, ids, use_rccl); });
+    for (int r = 0; r < cfg.ranks; ++r) th.emplace_back([&, r] { guarded(r); });
     for (auto& t : th) t.join();
   }
   return sh.rep;

@@ -40,7 +40,8 @@ class GaussJordan:
     ranks: int = 1
     device: str = "auto"
     dtype: str = "fp64"
-    comm: str = "auto"
+    comm: str = "auto"  # auto | rccl | loopback | async (stream-ordered virtual ranks)
+    jitter_us: float = 0.0  # comm="async": random per-rank arrival delays (race screening)
     chunk_cols: int = 0
     depth: int = 0  # 0 = auto (2 up to N=8192, else 4)
     eps: float = 1e-15
@@ -55,7 +56,7 @@ class GaussJordan:
                    dtype=self.dtype, comm=self.comm, chunk_cols=int(self.chunk_cols), depth=int(self.depth),
                    eps=float(self.eps),
                    sync_debug=bool(self.sync_debug), residual=self.residual,
-                   host_threads=int(self.host_threads))
+                   host_threads=int(self.host_threads), jitter_us=float(self.jitter_us))
         cfg.update(self.extra)
         return cfg
 

@@ -99,7 +99,7 @@ def test_axb_and_profile_on_gpu(native, ranks):
     assert ph["trailing_update"]["ms"] > 0 and ph["pivot_search"]["calls"] == (n + m - 1) // m
 
 
-@pytest.mark.parametrize("variant", ["panel", "sweep"])
+@pytest.mark.parametrize("variant", ["panel", "sweep", "panel1", "panel_lds", "panel_rl"])
 def test_block_inverse_variants_in_engine(native, variant):
     n, m = 640, 128
     A = generate_matrix(n, "random", 21)[::-1].copy()  # forces off-diagonal pivots
@@ -159,3 +159,32 @@ def test_direct_bcast_loopback_ranks_on_one_gpu(p, monkeypatch):
     assert np.array_equal(ring, direct)
     ref = np.linalg.inv(A)
     assert np.abs(direct - ref).max() / np.abs(ref).max() < 1e-8
+
+
+@pytest.mark.parametrize("p", [2, 3, 4, 8])
+@pytest.mark.parametrize("jitter", [0.0, 200.0])
+def test_async_ranks_on_one_gpu(p, jitter):
+    """Stream-ordered virtual ranks on one GPU (AsyncLoopbackComm): collectives are event waits
+    between the ranks' HIP streams, no stream is ever drained, so COMM broadcasts really race MAIN
+    GEMMs as under RCCL.  Random per-rank delays (a spin kernel on the issuing stream + host sleeps)
+    reorder the arrivals.  Must match numpy and be bit-identical to the host-drained loopback."""
+    n, m = 700, 64
+    A = generate_matrix(n, "random", 9)[::-1].copy()
+    sync = gj.GaussJordan(block_size=m, ranks=p, device="gpu", comm="loopback", depth=2, chunk_cols=128).inverse(A)
+    asy = gj.GaussJordan(block_size=m, ranks=p, device="gpu", comm="async", jitter_us=jitter, depth=2,
+                         chunk_cols=128).inverse(A)
+    ref = np.linalg.inv(A)
+    assert np.abs(asy - ref).max() / np.abs(ref).max() < 1e-8
+    assert np.array_equal(asy, sync)
+
+
+@pytest.mark.parametrize("p", [3, 8])
+def test_async_ranks_direct_bcast_on_one_gpu(p, monkeypatch):
+    monkeypatch.setenv("GJ_BCAST", "direct")
+    monkeypatch.setenv("GJ_BCAST_MIN", "1")
+    n, m = 700, 64
+    A = generate_matrix(n, "random", 9)[::-1].copy()
+    asy = gj.GaussJordan(block_size=m, ranks=p, device="gpu", comm="async", jitter_us=100.0, depth=4,
+                         chunk_cols=192).inverse(A)
+    ref = np.linalg.inv(A)
+    assert np.abs(asy - ref).max() / np.abs(ref).max() < 1e-8
