@@ -46,7 +46,12 @@ def main() -> int:
                     help="pivot-row broadcast at p > 2 (default: GJ_BCAST or auto = both timed at "
                          "engine setup, the faster kept)")
     ap.add_argument("--gemm-variant", default=None, help="big | narrow | tall (kernel tile config)")
+    ap.add_argument("--device", choices=["gpu", "cpu"], default="gpu",
+                    help="cpu = the native host executor with gloo collectives (rehearses the exact "
+                         "multi-rank script on a machine without GPUs; not a performance mode)")
+    ap.add_argument("--host-threads", type=int, default=1, help="host executor threads per rank (--device cpu)")
     args = ap.parse_args()
+    gpu = args.device == "gpu"
 
     # One hardware queue per stream: the engine's MAIN/SIDE/COMM streams plus torch's and RCCL's own
     # streams exceed HIP's default of 4, and streams that share a hardware queue also share its
@@ -71,10 +76,22 @@ def main() -> int:
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         return 2
-    torch.cuda.set_device(local)
+    if gpu:
+        torch.cuda.set_device(local)
     if args.gemm_variant:
         C.set_gemm_variant(args.gemm_variant)
-    if world > 1 or args.force_rccl:
+    if not gpu:
+        dev = C.host_device(args.host_threads)
+        if world > 1:
+            from mpi_jordan_crazy_acceleration_amd.parallel.dist import TorchDistComm
+
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            comm = C.py_comm(TorchDistComm(), rank, world)
+        else:
+            comm = C.self_comm()
+    elif world > 1 or args.force_rccl:
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29533")
@@ -86,12 +103,19 @@ def main() -> int:
     else:
         dev = C.hip_device(local)
         comm = C.self_comm()
-    eng = C.Engine(dev, comm, args.n, args.m, args.dtype, args.chunk_cols, 1e-15, False, args.depth)
+    try:
+        # allocation is agreed on every rank inside the constructor (a rank that cannot allocate
+        # makes every rank fail here, before any other collective)
+        eng = C.Engine(dev, comm, args.n, args.m, args.dtype, args.chunk_cols, 1e-15, False, args.depth)
+    except RuntimeError as e:
+        print(f"bench.py: rank {rank}: {e}", file=sys.stderr, flush=True)
+        return 2
 
     def barrier():
         if dist.is_initialized():
             dist.barrier()
-        torch.cuda.synchronize()
+        if gpu:
+            torch.cuda.synchronize()
 
     def step():
         eng.generate(args.gen, args.seed)
@@ -100,7 +124,7 @@ def main() -> int:
     for _ in range(args.warmup):
         st = step()
         if st["status"] != 0:
-            print(f"bench.py: solve failed with status {st['status']}", file=sys.stderr)
+            print(f"bench.py: rank {rank}: solve failed with status {st['status']}", file=sys.stderr)
             return 2
     barrier()
     t0 = time.perf_counter()
@@ -112,7 +136,7 @@ def main() -> int:
     t1 = time.perf_counter()
     ms = (t1 - t0) * 1e3 / max(args.steps, 1)
     if dist.is_initialized():
-        t = torch.tensor([ms, max(inner)], dtype=torch.float64, device="cuda")
+        t = torch.tensor([ms, max(inner)], dtype=torch.float64, device="cuda" if gpu else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ms, inner_max = float(t[0]), float(t[1])
     else:
@@ -134,13 +158,15 @@ def main() -> int:
             "scaling": "strong",
             "vs_baseline": round(gflops / REFERENCE_GFLOPS, 2),
             "dtype": args.dtype,
-            "data": "synthetic: seeded uniform[-1,1) dense random matrix generated on-GPU each step",
+            "data": "synthetic: seeded uniform[-1,1) dense random matrix generated on-"
+                    + ("GPU" if gpu else "host (--device cpu rehearsal)") + " each step",
             "config": {
                 "model": f"dense block Gauss-Jordan inversion N={args.n} (block m={args.m}, in-place, "
                          "min-inverse-norm block pivoting)",
                 "global_batch": 1,
                 "seq_len": args.n,
-                "parallelism": f"block-row-cyclic p={world} (RCCL over xGMI)" if world > 1 else "single GPU",
+                "parallelism": (f"block-row-cyclic p={world} (" + ("RCCL over xGMI" if gpu else "gloo, host executor")
+                                + ")") if world > 1 else ("single GPU" if gpu else "single host rank"),
                 "n": args.n,
                 "m": args.m,
                 "depth": eng.layout["depth"],

@@ -185,9 +185,10 @@ int main(int argc, char* argv[]) {
     case Status::CannotRead: std::printf("%s\n", rep.message.c_str()); return 2;
     case Status::NoMemory: std::printf("Not enough memory!\n"); if (!rep.message.empty()) std::fprintf(stderr, "%s\n", rep.message.c_str()); return 2;
     case Status::Singular:
+    case Status::NoBlockMemory:  // both are Jordan() failures: after the A corner (main.cpp:410-443)
       std::printf("A\n");
       print_corner(stdout, rep.corner_a, (int)std::min<long long>(n, cfg.print_max));
-      std::printf("singular matrix\n");
+      std::printf(rep.status == Status::Singular ? "singular matrix\n" : "not enough memory for block\n");
       if (json) json_report(cfg, rep);
       return 2;
     default: std::printf("error: %s\n", rep.message.c_str()); return 2;

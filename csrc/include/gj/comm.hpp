@@ -80,10 +80,21 @@ class Comm {
   // device-side collectives blocked on a dead peer return.
   virtual void check_health() {}
   virtual void abort() {}
+  // Host wait for stream s (all streams) with failure detection: the stream is polled, the
+  // transport checked every 20 ms, and after timeout() seconds the transport is aborted and
+  // Error(CommError) thrown.  Every host wait that can sit behind a collective goes through here:
+  // a plain hipStreamSynchronize behind a collective with a dead peer never returns.
+  void drain(Device& dev, int s);
+  void drain_all(Device& dev);
+  void set_timeout(double seconds) { timeout_s_ = seconds; }
+  double timeout() const { return timeout_s_; }
 
  protected:
+  double timeout_s_ = 600;
   // Whether GJ_BCAST=auto measures (a GPU transport whose two algorithms differ in cost).
   virtual bool tunable() const { return false; }
+  // Whether bcast_direct moves real data (false for the timing emulation, whose peers are synthetic).
+  virtual bool direct_capable() const { return true; }
   bool use_direct(size_t bytes) const { return direct_min_ > 0 && size() > 2 && bytes >= direct_min_; }
   void bcast_direct(Device& dev, const std::vector<BcastOp>& ops, int s);
   size_t direct_min_ = 0;

@@ -32,11 +32,12 @@ inline const char* dtype_name(DType t) { return t == DType::F64 ? "fp64" : "fp32
 enum class Status : int {
   Ok = 0,
   Singular = 1,        // "singular matrix"
-  NoMemory = 2,        // "not enough memory for block"
+  NoMemory = 2,        // "Not enough memory!" (the matrix itself does not fit, main.cpp:366-381)
   CannotOpen = 3,      // "cannot open %s"
   CannotRead = 4,      // "cannot read %s"
   BadArgs = 5,
   CommError = 6,
+  NoBlockMemory = 7,   // "not enough memory for block" (the elimination work space, main.cpp:428-436)
 };
 
 class Error : public std::runtime_error {

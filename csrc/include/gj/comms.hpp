@@ -171,6 +171,9 @@ class ShadowComm : public Comm {
   void host_allgather(Device& dev, const void* send, void* recv, size_t bytes) override;
   void reset() { step_ = 0; }
 
+ protected:
+  bool direct_capable() const override { return false; }
+
  private:
   int p_;
   int64_t step_ = 0;

@@ -88,6 +88,9 @@ class Device {
   virtual bool query_event(int ev) = 0;  // true once all work before the record has completed
   virtual void sync_stream(int s) = 0;
   virtual void sync_all() = 0;
+  // Non-blocking: true once everything enqueued on stream s has completed (Comm::drain polls it so
+  // that a host wait behind a collective can notice a dead peer).  Synchronous devices: always true.
+  virtual bool stream_idle(int s) { sync_stream(s); return true; }
   virtual float event_ms(int ev_start, int ev_end) = 0;
   virtual void* native_stream(int s) = 0;  // hipStream_t (nullptr on host)
   // Cross-device ordering points (the asynchronous virtual-rank transport, AsyncLoopbackComm):

@@ -125,7 +125,10 @@ class Engine {
 
  private:
   static constexpr int kMaxDepth = GemmExtra::kMaxZeroRows;
-  void alloc_buffers();
+  // 0 = ok, 1 = the work space does not fit, 2 = the matrix panels do not fit (why: the reason)
+  int alloc_buffers(std::string& why);
+  void alloc_work(int64_t wmax);
+  void free_work();     // everything but the matrix panels
   void free_buffers();
   // Pivot search for step t on the multiplier segment Lt (SIDE stream); result -> piv_host_[t&1].
   void select(int64_t t, const void* Lt);
@@ -216,6 +219,10 @@ class Engine {
   std::vector<PMark> pmarks_;
   bool solved_ = false;
   bool two_main_ = false;
+  // The work space did not fit on some rank (agreed at construction): solve() reports
+  // Status::NoBlockMemory, the reference's "not enough memory for block" (main.cpp:428-436).
+  bool block_mem_fail_ = false;
+  std::string block_mem_why_;
 };
 
 }  // namespace gj

@@ -38,6 +38,7 @@ class HipDevice : public Device {
  public:
   int reserve_cus(int n, int mode) override;
   void sync_stream(int s) override;
+  bool stream_idle(int s) override;
   void sync_all() override;
   float event_ms(int ev_start, int ev_end) override;
   void* native_stream(int s) override;

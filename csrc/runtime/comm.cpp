@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gj/comm.hpp"
@@ -72,16 +73,55 @@ void Comm::bcast_direct(Device& dev, const std::vector<BcastOp>& ops, int s) {
   group_p2p(dev, ph, s);
 }
 
+void Comm::drain(Device& dev, int s) {
+  if (size() == 1 || !dev.on_gpu()) {
+    dev.sync_stream(s);
+    return;
+  }
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  auto next = t0 + std::chrono::milliseconds(20);
+  int spins = 0;
+  while (!dev.stream_idle(s)) {
+    if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    const auto t = clk::now();
+    if (t < next) continue;
+    check_health();
+    if (std::chrono::duration<double>(t - t0).count() > timeout_s_) {
+      abort();
+      throw Error(Status::CommError, "timed out after " + std::to_string(timeout_s_) +
+                                         " s waiting for stream " + std::to_string(s) +
+                                         " behind a collective (peer failure or hang)");
+    }
+    next = t + std::chrono::milliseconds(20);
+  }
+}
+
+void Comm::drain_all(Device& dev) {
+  for (int s = 0; s < kNumStreams; ++s) drain(dev, s);
+}
+
 std::string Comm::tune_bcast(Device& dev, size_t bytes) { return tune_bcast(dev, std::vector<size_t>{bytes}); }
 
 std::string Comm::tune_bcast(Device& dev, std::vector<size_t> sizes) {
   const char* e = std::getenv("GJ_BCAST");
   const std::string mode = (e && *e) ? e : "auto";
   GJ_REQUIRE(mode == "auto" || mode == "ring" || mode == "direct", "GJ_BCAST must be ring|direct|auto");
-  const size_t mn = std::max<size_t>(1, env_size("GJ_BCAST_MIN", size_t(64) << 10));
+  size_t mn = std::max<size_t>(1, env_size("GJ_BCAST_MIN", size_t(64) << 10));
   direct_min_ = 0;
-  if (size() <= 2 || mode == "ring") {
+  if (size() <= 2) {  // the two algorithms coincide
     bcast_report_ = "ring";
+    return "ring";
+  }
+  // Every rank reads its own environment: a rank sending direct while a peer sends ring would hang
+  // both, so the mode and the threshold are agreed first (a mismatch is an error on every rank).
+  const double code = mode == "ring" ? 0.0 : mode == "direct" ? 1.0 : 2.0;
+  const double lo_code = -host_max(dev, -code), hi_code = host_max(dev, code);
+  const double lo_mn = -host_max(dev, -(double)mn), hi_mn = host_max(dev, (double)mn);
+  if (lo_code != hi_code || lo_mn != hi_mn)
+    throw Error(Status::BadArgs, "GJ_BCAST / GJ_BCAST_MIN differ between ranks");
+  if (mode == "ring" || !direct_capable()) {
+    bcast_report_ = direct_capable() ? "ring" : "ring (transport has no point-to-point path)";
     return "ring";
   }
   if (mode == "direct") {
@@ -101,17 +141,21 @@ std::string Comm::tune_bcast(Device& dev, std::vector<size_t> sizes) {
   const int s = S_COMM;
   const size_t maxb = sizes.back();
   void* buf = dev.alloc(maxb);
-  // bit-exact delivery check of the direct path (root 1, so the root's own slice index is skipped)
+  // bit-exact delivery check of the direct path on BOTH communicators (COMM carries the row
+  // segments, SIDE the panel pieces; root 1, so the root's own slice index is skipped)
   std::vector<uint32_t> pat(maxb / 4 + 1), got(maxb / 4 + 1);
   for (size_t i = 0; i < pat.size(); ++i) pat[i] = (uint32_t)(i * 2654435761u) ^ 0x5bd1e995u;
   const int vroot = 1 % p;
-  if (me == vroot) dev.copy(buf, pat.data(), maxb, s);
-  else dev.memset0(buf, maxb, s);
-  dev.sync_stream(s);
-  bcast_direct(dev, {BcastOp{buf, maxb, vroot}}, s);
-  dev.copy(got.data(), buf, maxb, s);
-  dev.sync_stream(s);
-  const bool ok_local = std::memcmp(got.data(), pat.data(), maxb) == 0;
+  bool ok_local = true;
+  for (int cs : {S_COMM, S_SIDE}) {
+    if (me == vroot) dev.copy(buf, pat.data(), maxb, cs);
+    else dev.memset0(buf, maxb, cs);
+    drain(dev, cs);
+    bcast_direct(dev, {BcastOp{buf, maxb, vroot}}, cs);
+    dev.copy(got.data(), buf, maxb, cs);
+    drain(dev, cs);
+    ok_local = ok_local && std::memcmp(got.data(), pat.data(), maxb) == 0;
+  }
   const bool ok = host_max(dev, ok_local ? 0.0 : 1.0) == 0.0;
   auto time_algo = [&](bool direct, size_t bytes) {
     auto run = [&](int it) {
@@ -120,12 +164,12 @@ std::string Comm::tune_bcast(Device& dev, std::vector<size_t> sizes) {
       else bcast(dev, o.buf, o.bytes, o.root, s);
     };
     for (int it = 0; it < 2; ++it) run(it);
-    dev.sync_stream(s);
+    drain(dev, s);
     host_max(dev, 0.0);  // barrier
     const auto t0 = std::chrono::steady_clock::now();
     const int iters = 2 * p;
     for (int it = 0; it < iters; ++it) run(it);
-    dev.sync_stream(s);
+    drain(dev, s);
     const double ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / iters;
     return host_max(dev, ms);

@@ -156,6 +156,12 @@ bool HipDevice::query_event(int ev) {
   return true;
 }
 void HipDevice::sync_stream(int s) { HIP_OK(hipStreamSynchronize(hs(streams_[s]))); }
+bool HipDevice::stream_idle(int s) {
+  const hipError_t e = hipStreamQuery(hs(streams_[s]));
+  if (e == hipErrorNotReady) return false;
+  HIP_OK(e);
+  return true;
+}
 void HipDevice::sync_all() {
   for (int s = 0; s < kNumStreams; ++s) sync_stream(s);
 }

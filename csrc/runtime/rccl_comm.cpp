@@ -130,20 +130,20 @@ void RcclComm::abort() {
 }
 
 void RcclComm::barrier(Device& dev) {
-  dev.sync_all();
+  drain_all(dev);
   double v = 0.0;
   host_max(dev, v);
 }
 
 double RcclComm::host_max(Device& dev, double v) {
   (void)hipSetDevice(device_);
-  dev.sync_stream(S_SIDE);
+  drain(dev, S_SIDE);
   double* d = static_cast<double*>(dbuf_);
   dev.copy(d, &v, sizeof(double), S_SIDE);
   allreduce_max(dev, d, 1, S_SIDE);
   double out = 0;
   dev.copy(&out, d, sizeof(double), S_SIDE);
-  dev.sync_stream(S_SIDE);
+  drain(dev, S_SIDE);
   return out;
 }
 
@@ -157,11 +157,11 @@ void RcclComm::host_allgather(Device& dev, const void* send, void* recv, size_t 
     owned = true;
   }
   char* d = static_cast<char*>(tmp);
-  dev.sync_stream(S_SIDE);
+  drain(dev, S_SIDE);
   dev.copy(d, send, bytes, S_SIDE);
   allgather(dev, d, d + bytes, bytes, S_SIDE);
   dev.copy(recv, d + bytes, bytes * n_, S_SIDE);
-  dev.sync_stream(S_SIDE);
+  drain(dev, S_SIDE);
   if (owned) (void)hipFree(tmp);
 }
 

@@ -64,11 +64,28 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   for (size_t c = 0; c < cb0_.size(); ++c)
     for (int64_t b = cb0_[c]; b < cb1_[c]; ++b) chunk_of_[b] = (int64_t)c;
 
-  alloc_buffers();
+  comm_.set_timeout(opt_.comm_timeout_s);
+  // Allocation, agreed on every rank BEFORE any other collective (reference main.cpp:366-381 and
+  // :428-436): 2 = this rank's matrix panels do not fit ("Not enough memory!", thrown on every
+  // rank), 1 = the elimination work space does not ("not enough memory for block", reported by
+  // solve() on every rank), 0 = ok.  With Nr % p != 0 the low ranks own one more block row, so near
+  // the HBM limit a single rank can fail alone; its peers must not run on into the broadcast tuner.
+  std::string why;
+  const int mine = alloc_buffers(why);
+  const int agreed = (int)comm_.host_max(dev_, (double)mine);
+  if (agreed == 2) {
+    free_buffers();
+    throw Error(Status::NoMemory, mine == 2 ? why : "not enough device memory on a peer rank");
+  }
+  if (agreed == 1) {
+    free_work();
+    block_mem_fail_ = true;
+    block_mem_why_ = mine == 1 ? why : "not enough device memory for the work space on a peer rank";
+  }
   // Broadcast algorithm for the panel pieces (m x d*m) and the pivot-row segments (m x chunk width):
   // ring or direct, measured here
   // on a GPU transport at p > 2 (Comm::tune_bcast; every rank takes the same decision).
-  {
+  if (!block_mem_fail_) {
     int64_t wmax = 0;
     for (size_t c = 0; c < cb0_.size(); ++c) wmax = std::max(wmax, chunk_w((int64_t)c));
     const size_t pp_bytes = (size_t)L_.m * d_ * L_.m * esz();  // panel piece (SIDE, pivot chain)
@@ -106,22 +123,62 @@ int64_t Engine::real_local_rows() const {
   return L_.rows - (last_global_block == L_.Nr - 1 ? (L_.m - L_.l_h) : 0);
 }
 
-void Engine::alloc_buffers() {
+namespace {
+// GJ_TEST_ALLOC_FAIL=<rank>:<matrix|block> makes that rank's allocation fail (failure-agreement tests).
+bool injected_alloc_fail(int rank, const char* stage) {
+  const char* e = std::getenv("GJ_TEST_ALLOC_FAIL");
+  if (!e || !*e) return false;
+  const std::string v = e;
+  const size_t c = v.find(':');
+  return c != std::string::npos && std::atoi(v.substr(0, c).c_str()) == rank && v.substr(c + 1) == stage;
+}
+}  // namespace
+
+int Engine::alloc_buffers(std::string& why) {
   const int64_t m = L_.m, rows = std::max<int64_t>(L_.rows, 1), npad = L_.npad, dm = (int64_t)d_ * m;
   const size_t es = esz();
   const size_t panel = (size_t)rows * npad * es;
   int64_t wmax = 0;
   for (size_t c = 0; c < cb0_.size(); ++c) wmax = std::max(wmax, chunk_w((int64_t)c));
-  const size_t need = 2 * panel + 3 * (size_t)dm * rows * es + 2 * (size_t)dm * npad * es +
-                      (size_t)std::max<int64_t>(L_.nblk, 1) * m * m * es + (size_t)m * wmax * es;
-  if (dev_.on_gpu()) {
-    size_t avail = dev_.free_memory();
-    if (need + (64u << 20) > avail)
-      throw Error(Status::NoMemory, "not enough device memory: need " + std::to_string(need) +
-                                        " bytes, have " + std::to_string(avail));
+  const size_t need_matrix = 2 * panel;
+  const size_t need_work = 3 * (size_t)dm * rows * es + 2 * (size_t)dm * npad * es +
+                           (size_t)std::max<int64_t>(L_.nblk, 1) * m * m * es + (size_t)m * wmax * es;
+  const size_t avail = dev_.on_gpu() ? dev_.free_memory() : SIZE_MAX;
+  auto fits = [&](size_t need) { return !dev_.on_gpu() || need + (64u << 20) <= avail; };
+  // stage 1: the matrix panels (the reference's a / b arrays)
+  try {
+    if (injected_alloc_fail(L_.k, "matrix")) throw Error(Status::NoMemory, "injected (GJ_TEST_ALLOC_FAIL)");
+    if (!fits(need_matrix))
+      throw Error(Status::NoMemory, "not enough device memory: the matrix panels need " +
+                                        std::to_string(need_matrix) + " bytes, have " + std::to_string(avail));
+    X_ = dev_.alloc(panel);
+    out_ = dev_.alloc(panel);
+  } catch (const Error& e) {
+    if (e.status() != Status::NoMemory) throw;
+    why = e.what();
+    free_buffers();
+    return 2;
   }
-  X_ = dev_.alloc(panel);
-  out_ = dev_.alloc(panel);
+  // stage 2: the elimination work space (the reference's per-step block buffers, main.cpp:960-975)
+  try {
+    if (injected_alloc_fail(L_.k, "block")) throw Error(Status::NoMemory, "injected (GJ_TEST_ALLOC_FAIL)");
+    if (!fits(need_matrix + need_work))
+      throw Error(Status::NoMemory, "not enough device memory: the work space needs " +
+                                        std::to_string(need_work) + " bytes beyond the matrix, have " +
+                                        std::to_string(avail));
+    alloc_work(wmax);
+  } catch (const Error& e) {
+    if (e.status() != Status::NoMemory) throw;
+    why = e.what();
+    free_work();
+    return 1;
+  }
+  return 0;
+}
+
+void Engine::alloc_work(int64_t wmax) {
+  const int64_t m = L_.m, rows = std::max<int64_t>(L_.rows, 1), npad = L_.npad, dm = (int64_t)d_ * m;
+  const size_t es = esz();
   for (int i = 0; i < 3; ++i) At_[i] = dev_.alloc((size_t)dm * rows * es);
   for (int i = 0; i < 2; ++i) {
     Rb_[i] = dev_.alloc((size_t)dm * npad * es);
@@ -150,6 +207,7 @@ void Engine::alloc_buffers() {
   ihost_ = static_cast<int32_t*>(dev_.alloc_pinned(sizeof(int32_t) * ihost_len_));
   dhost_ = static_cast<double*>(dev_.alloc_pinned(sizeof(double) * 64));
 
+  if (ev_L_ >= 0) return;  // events are the device's; created once
   ev_L_ = dev_.create_event();
   ev_main_ = dev_.create_event();
   ev_main2_ = dev_.create_event();
@@ -162,27 +220,47 @@ void Engine::alloc_buffers() {
   for (size_t c = 0; c < cb0_.size(); ++c) ev_c_.push_back(dev_.create_event());
 }
 
-void Engine::free_buffers() {
-  std::vector<void*> dptrs = {X_, out_, T_, RP_, inv_, scores_, valid_, pos_, phys_at_, used_, seq_,
-                              myrec_, recs_, piv_dev_, dscratch_, iscratch_};
-  for (int i = 0; i < 3; ++i) dptrs.push_back(At_[i]);
+void Engine::free_work() {
+  std::vector<void**> dptrs = {&T_, &RP_, &inv_, reinterpret_cast<void**>(&scores_),
+                               reinterpret_cast<void**>(&valid_), reinterpret_cast<void**>(&pos_),
+                               reinterpret_cast<void**>(&phys_at_), reinterpret_cast<void**>(&used_),
+                               reinterpret_cast<void**>(&seq_), reinterpret_cast<void**>(&myrec_),
+                               reinterpret_cast<void**>(&recs_), reinterpret_cast<void**>(&piv_dev_),
+                               reinterpret_cast<void**>(&dscratch_), reinterpret_cast<void**>(&iscratch_)};
+  for (int i = 0; i < 3; ++i) dptrs.push_back(&At_[i]);
   for (int i = 0; i < 2; ++i) {
-    dptrs.push_back(Rb_[i]);
-    dptrs.push_back(PP_[i]);
+    dptrs.push_back(&Rb_[i]);
+    dptrs.push_back(&PP_[i]);
     for (int j = 0; j < kMaxDepth; ++j) {
-      dptrs.push_back(Lrow_[i][j]);
-      dptrs.push_back(Ht_[i][j]);
+      dptrs.push_back(&Lrow_[i][j]);
+      dptrs.push_back(&Ht_[i][j]);
     }
   }
-  for (void* p : dptrs)
-    if (p) dev_.release(p);
-  if (piv_host_) dev_.release_pinned(piv_host_);
-  if (ihost_) dev_.release_pinned(ihost_);
-  if (dhost_) dev_.release_pinned(dhost_);
+  for (void** p : dptrs)
+    if (*p) {
+      dev_.release(*p);
+      *p = nullptr;
+    }
+  std::vector<void**> hptrs = {reinterpret_cast<void**>(&piv_host_), reinterpret_cast<void**>(&ihost_),
+                               reinterpret_cast<void**>(&dhost_)};
+  for (void** p : hptrs)
+    if (*p) {
+      dev_.release_pinned(*p);
+      *p = nullptr;
+    }
+}
+
+void Engine::free_buffers() {
+  free_work();
+  for (void** p : {&X_, &out_})
+    if (*p) {
+      dev_.release(*p);
+      *p = nullptr;
+    }
 }
 
 void Engine::dbg_sync() {
-  if (opt_.sync_debug) dev_.sync_all();
+  if (opt_.sync_debug) comm_.drain_all(dev_);
 }
 
 const char* phase_name(int ph) {
@@ -383,7 +461,7 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
     wait_pivot((int)(t & 1), t, host_wait);
     const PivotResult r = piv_host_[t & 1];
     if (!r.found) {
-      dev_.sync_all();
+      comm_.drain_all(dev_);
       st.status = Status::Singular;
       st.singular_step = t;
       return false;
@@ -605,6 +683,11 @@ SolveStats Engine::solve() {
   const int64_t m = L_.m, Nr = L_.Nr, rows = L_.rows, npad = L_.npad;
   pmarks_.clear();
   pev_next_ = 0;
+  if (block_mem_fail_) {  // agreed at construction: the same answer on every rank, no collective
+    st.status = Status::NoBlockMemory;
+    solved_ = true;
+    return st;
+  }
 
   comm_.barrier(dev_);
   const double t_begin = now_s();
@@ -640,7 +723,7 @@ SolveStats Engine::solve() {
     if (u + 1 < npanels()) ok = factor_panel(u + 1, /*wait_main=*/true, st, host_wait);
   }
   if (!ok) {
-    dev_.sync_all();
+    comm_.drain_all(dev_);
     st.host_wait_ms = host_wait * 1e3;
     st.seconds = now_s() - t_begin;
     solved_ = true;
@@ -656,7 +739,7 @@ SolveStats Engine::solve() {
     finalize(st.pivots);
     prof_end(PH_FINALIZE, pe, S_COMM);
   }
-  dev_.sync_all();
+  comm_.drain_all(dev_);
   const double t_end = now_s();
   for (int64_t t = 0; t < Nr; ++t)
     if (st.pivots[t] != t) st.offdiag_pivots++;
@@ -708,7 +791,7 @@ void Engine::finalize(const std::vector<int32_t>& seq) {
     }
   }
   comm_.group_p2p(dev_, ops, S_COMM);
-  dev_.sync_stream(S_COMM);
+  comm_.drain(dev_, S_COMM);
   std::swap(X_, out_);
 }
 
@@ -772,6 +855,13 @@ double Engine::residual_common() {
   void* gath = nullptr;
   if (p > 1) {
     const size_t per = (size_t)L_.max_nblk * m * npad * es;
+    // the whole inverse on every rank: agree that it fits everywhere before the first allocation
+    const size_t need = (size_t)npad * npad * es + per * p + (L_.nblk < L_.max_nblk ? per : 0);
+    const bool fits = !injected_alloc_fail(L_.k, "residual") &&
+                      (!dev_.on_gpu() || need + (64u << 20) <= dev_.free_memory());
+    if (comm_.host_max(dev_, fits ? 0.0 : 1.0) > 0)
+      throw Error(Status::NoMemory, "not enough device memory for the residual's gathered inverse (" +
+                                        std::to_string(need) + " bytes per rank)");
     full = dev_.alloc((size_t)npad * npad * es);
     gath = dev_.alloc(per * p);
     void* send = out_;
@@ -790,7 +880,7 @@ double Engine::residual_common() {
                   static_cast<char*>(gath) + q * per + (size_t)j * m * npad * es,
                   (size_t)m * npad * es, S_COMM);
     }
-    dev_.sync_stream(S_COMM);
+    comm_.drain(dev_, S_COMM);
     if (tmp) dev_.release(tmp);
     dev_.release(gath);
   }

@@ -129,7 +129,7 @@ void rank_main(const RunConfig& cfg, int rank, Shared& sh, std::shared_ptr<Loopb
   if (st.status != Status::Ok) {
     std::lock_guard<std::mutex> lk(sh.mu);
     sh.rep.status = st.status;
-    sh.rep.message = "singular matrix";
+    sh.rep.message = st.status == Status::NoBlockMemory ? "not enough memory for block" : "singular matrix";
     if (rank == 0) sh.rep.stats = st;
     return;
   }
