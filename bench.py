@@ -53,20 +53,18 @@ def main() -> int:
     args = ap.parse_args()
     gpu = args.device == "gpu"
 
-    # One hardware queue per stream: the engine's MAIN/SIDE/COMM streams plus torch's and RCCL's own
-    # streams exceed HIP's default of 4, and streams that share a hardware queue also share its
-    # in-order barrier packets (a cross-stream event wait then stalls unrelated work).  Must be set
-    # before the first HIP call of the process.
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
-    # Kernel arguments in device memory: measured 0 vs 1 on one box, N = 8192 31.3 vs 30.2 ms
-    # (profiles/small_n_sweep.md); pinned in case a runtime's default differs.
-    os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+    # Hardware queues and kernel-argument placement, before the first HIP call of the process
+    # (mpi_jordan_crazy_acceleration_amd/runtime_env.py: one queue per stream, so the two RCCL
+    # communicators' kernels never queue behind each other; device-memory kernel arguments).
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from mpi_jordan_crazy_acceleration_amd.runtime_env import configure_runtime_env
+
+    configure_runtime_env()
     if args.bcast:
         os.environ["GJ_BCAST"] = args.bcast
     import torch
     import torch.distributed as dist
 
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from mpi_jordan_crazy_acceleration_amd import load_native
 
     C = load_native()

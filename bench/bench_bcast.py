@@ -21,7 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mib", type=float, nargs="+", default=[0.5, 2, 8, 32])
     args = ap.parse_args()
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    os.environ["GPU_MAX_HW_QUEUES"] = str(max(16, int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))))
     os.environ["GJ_BCAST"] = "auto"
     import torch
     import torch.distributed as dist

@@ -2,11 +2,14 @@
 """Per-rank critical-path emulation of a p-GPU solve on ONE GPU (ShadowComm, gj/comms.hpp).
 
 Rank 0 of a p-rank job runs alone: 1/p of the rows, all pivot searches, panel pieces, chunk
-pipeline and full-width trailing updates; peers' rows arrive as zeros and broadcasts are local, so
-the time is a LOWER bound of the real p-GPU step (xGMI transfer time excluded) and an UPPER bound
-check of whether the look-ahead hides the pivot path.  Not a headline number (see bench.py).
+pipeline and full-width trailing updates; peers' rows arrive as zeros.  Without --bw broadcasts are
+local (the time is a LOWER bound of the real p-GPU step, xGMI transfer time excluded).  With
+--bw GB/s every collective is replaced by its modelled cost (ShadowComm's CostModel: --lat us +
+bytes / bw on --channels spin workgroups of an RCCL channel's footprint, competing with the
+trailing update for CUs); "comm_hidden" is then the share of the modelled transfer time that the
+look-ahead hid: 1 - (t_model - t_free) / modelled.  Not a headline number (see bench.py).
 
-    python bench/bench_emulate.py --ranks 1 2 4 8 --size 32768
+    python bench/bench_emulate.py --ranks 1 2 4 8 --size 32768 [--bw 100 --lat 20]
 """
 import argparse
 import json
@@ -26,34 +29,55 @@ def main():
     ap.add_argument("--dtype", default="fp64")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--chunk-cols", type=int, default=0)
+    ap.add_argument("--bw", type=float, nargs="*", default=[],
+                    help="cost-model bandwidths in GB/s (each also runs the comm-free baseline)")
+    ap.add_argument("--lat", type=float, default=20.0, help="cost-model latency per collective, us")
+    ap.add_argument("--channels", type=int, default=16, help="cost-model workgroups per collective")
     args = ap.parse_args()
     import torch  # noqa: F401  (shares libamdhip64 with the extension)
     from mpi_jordan_crazy_acceleration_amd import load_native
 
     C = load_native()
     dev = C.hip_device(0)
+    def run(p, d, bw):
+        comm = (C.shadow_comm(p, bw, args.lat if bw > 0 else 0.0, args.channels) if p > 1
+                else C.self_comm())
+        eng = C.Engine(dev, comm, args.size, args.block, args.dtype, args.chunk_cols, 1e-15, False, d)
+        times, modelled = [], 0.0
+        for _ in range(args.reps + 1):
+            if p > 1:
+                C.shadow_reset(comm)
+                m0 = C.shadow_modelled_us(comm)
+            eng.generate("random", 7)
+            dev.sync()
+            t0 = time.perf_counter()
+            st = eng.solve()
+            dev.sync()
+            times.append(time.perf_counter() - t0)
+            if p > 1:
+                modelled = (C.shadow_modelled_us(comm) - m0) * 1e-6
+        rows = eng.layout["rows"]
+        del eng
+        return min(times[1:]), st, rows, modelled
+
     for p in args.ranks:
         for d in args.depth:
-            comm = C.shadow_comm(p) if p > 1 else C.self_comm()
-            eng = C.Engine(dev, comm, args.size, args.block, args.dtype, args.chunk_cols, 1e-15, False, d)
-            times = []
-            for _ in range(args.reps + 1):
-                if p > 1:
-                    C.shadow_reset(comm)
-                eng.generate("random", 7)
-                dev.sync()
-                t0 = time.perf_counter()
-                st = eng.solve()
-                dev.sync()
-                times.append(time.perf_counter() - t0)
-            t = min(times[1:])
-            rows = eng.layout["rows"]
+            t_free, st, rows, _ = run(p, d, 0.0)
             gemm_flops = 2.0 * rows * args.size * args.size  # this rank's share of 2N^3
             print(json.dumps({"p": p, "depth": d, "n": args.size, "m": args.block, "status": st["status"],
-                              "seconds": round(t, 4), "job_gflops_if_comm_free": round(2 * args.size ** 3 / t / 1e9, 1),
-                              "rank_tflops": round(gemm_flops / t / 1e12, 2),
+                              "seconds": round(t_free, 4),
+                              "job_gflops_if_comm_free": round(2 * args.size ** 3 / t_free / 1e9, 1),
+                              "rank_tflops": round(gemm_flops / t_free / 1e12, 2),
                               "host_wait_ms": round(st["host_wait_ms"], 1)}), flush=True)
-            del eng
+            for bw in (args.bw if p > 1 else []):
+                t, st, rows, modelled = run(p, d, bw)
+                hidden = 1.0 - (t - t_free) / modelled if modelled > 0 else None
+                print(json.dumps({"p": p, "depth": d, "n": args.size, "model_bw_gbs": bw, "model_lat_us": args.lat,
+                                  "model_channels": args.channels, "status": st["status"],
+                                  "seconds": round(t, 4),
+                                  "job_gflops_cost_model": round(2 * args.size ** 3 / t / 1e9, 1),
+                                  "modelled_comm_s": round(modelled, 4),
+                                  "comm_hidden": None if hidden is None else round(hidden, 3)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -85,6 +85,14 @@ static void json_report(const RunConfig& cfg, const RunReport& rep) {
 }
 
 int main(int argc, char* argv[]) {
+  // Before the first HIP call: one hardware queue per stream (the progress argument of the two RCCL
+  // communicators, README "Progress of the two communicators"; same policy as runtime_env.py) and
+  // kernel arguments in device memory.
+  {
+    const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+    if (!q || std::atoi(q) < kMinHwQueues) setenv("GPU_MAX_HW_QUEUES", std::to_string(kMinHwQueues).c_str(), 1);
+    setenv("HIP_FORCE_DEV_KERNARG", "1", 0);
+  }
   RunConfig cfg;
   std::vector<const char*> pos;
   bool json = false;

@@ -155,28 +155,47 @@ namespace gj {
 // the full-width trailing update) without p GPUs.  Peers are synthetic: at step t the pivot is
 // rank 0's own best candidate when t % p == 0, otherwise block row t (owned by rank t % p) with
 // a winning score; rows "received" from peers are zeros.  The inverse is meaningless; only the
-// timing is.  Communication time itself is NOT emulated (broadcasts are local memsets).
+// timing is.
+//
+// Communication-cost model (CostModel, off when bw_gbs <= 0): every collective occupies its
+// stream for  lat_us + bytes / bandwidth  on `channels` workgroups of a spin kernel of RCCL's
+// footprint (256 threads, lds_kib of LDS), so a transfer both takes time on its stream AND
+// competes with the trailing-update GEMM for CUs, as RCCL's channel workgroups do.  Bandwidth is
+// the per-broadcast algorithm bandwidth (a ring broadcast delivers the whole message to every
+// rank at the rate of its slowest hop); the final block exchange runs over min(p-1, 7) links.
+struct CostModel {
+  double bw_gbs = 0;     // broadcast / point-to-point algorithm bandwidth, GB/s (0 = free comm)
+  double lat_us = 0;     // per-collective latency (launch + handshake), us
+  int channels = 16;     // workgroups a collective holds while it runs
+  int lds_kib = 32;      // LDS per channel workgroup
+};
+
 class ShadowComm : public Comm {
  public:
-  explicit ShadowComm(int p) : p_(p) {}
+  explicit ShadowComm(int p, CostModel cm = CostModel()) : p_(p), cm_(cm) {}
   int size() const override { return p_; }
   int rank() const override { return 0; }
-  std::string describe() const override { return "shadow(" + std::to_string(p_) + ")"; }
+  std::string describe() const override;
   void allgather(Device& dev, const void* send, void* recv, size_t bytes, int s) override;
   void bcast(Device& dev, void* buf, size_t bytes, int root, int s) override;
   void allreduce_max(Device&, double*, size_t, int) override {}
-  void group_p2p(Device&, const std::vector<P2POp>&, int) override {}
+  void group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) override;
   void barrier(Device& dev) override { dev.sync_all(); }
   double host_max(Device&, double v) override { return v; }
   void host_allgather(Device& dev, const void* send, void* recv, size_t bytes) override;
   void reset() { step_ = 0; }
+  const CostModel& cost_model() const { return cm_; }
+  double modelled_us() const { return modelled_us_; }  // total modelled transfer time issued
 
  protected:
   bool direct_capable() const override { return false; }
 
  private:
+  void cost(Device& dev, size_t bytes, int links, int s);
   int p_;
+  CostModel cm_;
   int64_t step_ = 0;
+  double modelled_us_ = 0;
   std::vector<char> host_;
 };
 

@@ -103,7 +103,9 @@ class Device {
   // Timing / scheduling probes: keep stream s busy for `us` microseconds on `nwg` workgroups
   // (nwg = 1: a pure delay, e.g. per-rank start jitter; more: the CU footprint of a transfer in the
   // single-GPU communication-cost model of ShadowComm).  No-op where it has no meaning.
-  virtual void occupy(int s, int nwg, double us) { (void)s; (void)nwg; (void)us; }
+  virtual void occupy(int s, int nwg, double us, int lds_bytes = 0) {
+    (void)s; (void)nwg; (void)us; (void)lds_bytes;
+  }
   // Keep the MAIN (trailing-update) stream off `n` CUs so the latency-critical SIDE/COMM kernels
   // always find idle CUs (mode 0: CUs 0..n-1 of the mask, mode 1: spread over the mask).
   // Returns the number of CUs actually reserved.  Call while the device is idle.

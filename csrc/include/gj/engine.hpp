@@ -96,6 +96,9 @@ class Engine {
   // elements), copied device-to-device (e.g. straight from / into a torch CUDA tensor).
   void upload_rows_device(const void* src, int64_t ld);
   void download_rows_device(void* dst, int64_t ld);
+  // This rank's rows of a matrix file (text / .bin, read_matrix_rows): collective, every rank
+  // parses only its own rows.  Returns Ok, CannotOpen or CannotRead (the same on every rank).
+  Status load_file(const std::string& path, int nthreads = 0);
   // The input panel as it is right now (dtype elements, ld npad, layout().rows rows).
   void* input_panel() { return X_; }
   double norm_inf();  // collective
@@ -111,6 +114,8 @@ class Engine {
   // ||A * inv(A) - I||_inf  (collective).  The input panel is overwritten by A again.
   double residual_generated(GenSpec g);
   double residual_rows(const double* host, int64_t ld);
+  // Re-reads the file (reference main.cpp:463-484); *status = Ok / CannotOpen / CannotRead.
+  double residual_file(const std::string& path, int nthreads = 0, Status* status = nullptr);
 
   // ---- A x = b (BASELINE config 1; SURVEY.md §5.6 --rhs) ----
   // x = inv(A) b from the result panel: one MFMA GEMV per rank + all-gather (collective).
@@ -139,6 +144,7 @@ class Engine {
   void big_update(int64_t u);
   void finalize(const std::vector<int32_t>& seq);
   double residual_common();
+  Status read_file_rows(const std::string& path, int nthreads, std::vector<double>& rows);
   void dbg_sync();
   // Host wait for the pivot result of `step` (pinned slot par) with failure detection
   // (Comm::check_health + timeout).

@@ -44,7 +44,7 @@ class HipDevice : public Device {
   void* native_stream(int s) override;
   std::shared_ptr<void> mark(int s) override;
   void wait_mark(int s, const std::shared_ptr<void>& h) override;
-  void occupy(int s, int nwg, double us) override;
+  void occupy(int s, int nwg, double us, int lds_bytes = 0) override;
 
   void generate(DType dt, void* X, const Layout& L, GenSpec g, int s) override;
   void upload_convert(DType dt, void* X, int64_t ldx, const double* src_dev, int64_t src_ld,

@@ -17,6 +17,12 @@ namespace gj {
 // accept set as scanf("%lf").  Files ending in ".bin" are raw little-endian fp64 (n*n values).
 // Returns Ok, CannotOpen or CannotRead.  Parsing is parallel (nthreads, 0 = auto).
 Status read_matrix_file(const std::string& path, int64_t n, std::vector<double>& out, int nthreads = 0);
+// Only the given rows (global row indices, each at most once) of the n x n matrix, in that order:
+// out is rows.size() x n.  One rank's share in the one-process-per-GPU deployment: the file is
+// mapped and every rank parses only its own rows (peak memory ~ its share + a window per thread);
+// tokens of other rows are skipped, not validated (their owners validate them).
+Status read_matrix_rows(const std::string& path, int64_t n, const std::vector<int64_t>& rows,
+                        std::vector<double>& out, int nthreads = 0);
 // Same parser for the first `count` numbers (right-hand sides: count = n).
 Status read_values_file(const std::string& path, size_t count, std::vector<double>& out, int nthreads = 0);
 

@@ -48,8 +48,8 @@ void upload_convert(DType dt, void* X, int64_t ldx, const double* src, int64_t s
 void extract_neg_t(DType dt, void* Lt, int64_t ldl, const void* X, int64_t ldx, int64_t rows,
                    int64_t col0, int64_t m, hipStream_t s);
 void add_diag(DType dt, void* A, int64_t ld, int64_t nd, double alpha, hipStream_t s);
-// nwg one-wave workgroups that each spin for `us` microseconds
-void spin(int nwg, double us, hipStream_t s);
+// nwg workgroups that each spin for `us` microseconds (lds_bytes > 0: 256 threads + that much LDS)
+void spin(int nwg, double us, hipStream_t s, int lds_bytes = 0);
 void pivot_local(const double* scores, const int32_t* valid, const int32_t* used, const int32_t* pos,
                  const Layout& L, PivotRec* out, hipStream_t s);
 void pivot_select_single(const double* scores, const int32_t* valid, const Layout& L, int32_t t,

@@ -121,15 +121,17 @@ void extract_neg_t(DType dt, void* Lt, int64_t ldl, const void* X, int64_t ldx, 
 // Keep a stream busy for `ticks` of the 100 MHz wall clock on every launched workgroup (per-rank
 // start jitter of the asynchronous virtual ranks; the CU footprint of a transfer in ShadowComm's
 // communication-cost model).  Every wave leaves when the time is up.
-__global__ __launch_bounds__(64) void spin_kernel(uint64_t ticks) {
+// lds_bytes > 0: 256-thread workgroups holding that much LDS (the footprint of an RCCL channel).
+__global__ __launch_bounds__(256) void spin_kernel(uint64_t ticks) {
   const uint64_t t0 = wall_clock64();
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(4);
 }
 
-void spin(int nwg, double us, hipStream_t s) {
+void spin(int nwg, double us, hipStream_t s, int lds_bytes) {
   if (nwg <= 0 || !(us > 0)) return;
   const uint64_t ticks = (uint64_t)(us * 100.0);  // wall_clock64: 100 MHz
-  hipLaunchKernelGGL(spin_kernel, dim3((unsigned)nwg), dim3(64), 0, s, ticks);
+  const unsigned nt = lds_bytes > 0 ? 256u : 64u;
+  hipLaunchKernelGGL(spin_kernel, dim3((unsigned)nwg), dim3(nt), (size_t)(lds_bytes > 0 ? lds_bytes : 0), s, ticks);
 }
 
 template <typename T>

@@ -124,6 +124,21 @@ py::array_t<double> to_array(const std::vector<double>& v, int64_t r, int64_t c)
 PYBIND11_MODULE(_C, mod) {
   mod.doc() = "MI355X-native block Gauss-Jordan inversion: native engine, HIP kernels, RCCL comm";
 
+  // gj::Error -> GJError (a RuntimeError) carrying the engine status (2 = no memory for the matrix,
+  // 6 = communication failure, 7 = no memory for the work space, ...).
+  static py::object gj_error = py::reinterpret_steal<py::object>(
+      PyErr_NewException("mpi_jordan_crazy_acceleration_amd._C.GJError", PyExc_RuntimeError, nullptr));
+  mod.attr("GJError") = gj_error;
+  py::register_exception_translator([](std::exception_ptr p) {
+    try {
+      if (p) std::rethrow_exception(p);
+    } catch (const Error& e) {
+      py::object inst = gj_error(e.what());
+      inst.attr("status") = (int)e.status();
+      PyErr_SetObject(gj_error.ptr(), inst.ptr());
+    }
+  });
+
   mod.def("version", [] { return std::string("0.1.0"); });
   mod.def("device_count", [] {
     int n = 0;
@@ -272,12 +287,27 @@ PYBIND11_MODULE(_C, mod) {
             py::gil_scoped_release rel;
             return std::shared_ptr<Comm>(new RcclComm(s, nranks, rank, device));
           });
-  mod.def("shadow_comm", [](int p) { return std::shared_ptr<Comm>(new ShadowComm(p)); },
-          "rank 0 of a p-rank job alone on one device (critical-path timing emulation)");
+  mod.def("shadow_comm", [](int p, double bw_gbs, double lat_us, int channels, int lds_kib) {
+            CostModel cm;
+            cm.bw_gbs = bw_gbs;
+            cm.lat_us = lat_us;
+            cm.channels = channels;
+            cm.lds_kib = lds_kib;
+            return std::shared_ptr<Comm>(new ShadowComm(p, cm));
+          },
+          py::arg("p"), py::arg("bw_gbs") = 0.0, py::arg("lat_us") = 0.0, py::arg("channels") = 16,
+          py::arg("lds_kib") = 32,
+          "rank 0 of a p-rank job alone on one device (critical-path timing emulation); bw_gbs > 0 "
+          "adds the communication-cost model (lat_us + bytes/bw on `channels` spin workgroups)");
   mod.def("shadow_reset", [](std::shared_ptr<Comm> c) {
     auto* sc = dynamic_cast<ShadowComm*>(c.get());
     GJ_REQUIRE(sc != nullptr, "shadow_reset: not a shadow communicator");
     sc->reset();
+  });
+  mod.def("shadow_modelled_us", [](std::shared_ptr<Comm> c) {
+    auto* sc = dynamic_cast<ShadowComm*>(c.get());
+    GJ_REQUIRE(sc != nullptr, "shadow_modelled_us: not a shadow communicator");
+    return sc->modelled_us();
   });
   // Two virtual ranks on the host enter collectives with different roots (rank 1 passes root_b):
   // returns the error message the loopback consistency check raised on each rank ("" = none).
@@ -414,6 +444,24 @@ PYBIND11_MODULE(_C, mod) {
              return e.eng->residual_generated(g);
            },
            py::arg("kind") = "absdiff", py::arg("seed") = 0)
+      .def("load_file",
+           [](PyEngine& e, const std::string& path, int nthreads) {
+             py::gil_scoped_release rel;
+             return (int)e.eng->load_file(path, nthreads);
+           },
+           py::arg("path"), py::arg("nthreads") = 0,
+           "collective: this rank's rows of a matrix file; returns 0, 3 (cannot open) or 4 (cannot read)")
+      .def("residual_file",
+           [](PyEngine& e, const std::string& path, int nthreads) {
+             Status s = Status::Ok;
+             double r;
+             {
+               py::gil_scoped_release rel;
+               r = e.eng->residual_file(path, nthreads, &s);
+             }
+             return py::make_tuple((int)s, r);
+           },
+           py::arg("path"), py::arg("nthreads") = 0)
       .def("residual_rows", [](PyEngine& e, py::array_t<double, py::array::c_style | py::array::forcecast> a) {
         const int64_t real = e.eng->real_local_rows(), n = e.eng->layout().n;
         if (a.ndim() != 2 || a.shape(0) != real || a.shape(1) != n)
@@ -503,5 +551,17 @@ PYBIND11_MODULE(_C, mod) {
     if (s == Status::CannotOpen) throw std::runtime_error("cannot open " + path);
     if (s == Status::CannotRead) throw std::runtime_error("cannot read " + path);
     return to_array(v, n, n);
-  });
+  }, py::arg("path"), py::arg("n"));
+  mod.def("read_matrix_rows", [](const std::string& path, int64_t n, std::vector<int64_t> rows, int nthreads) {
+    std::vector<double> v;
+    Status s;
+    {
+      py::gil_scoped_release rel;
+      s = read_matrix_rows(path, n, rows, v, nthreads);
+    }
+    if (s == Status::CannotOpen) throw std::runtime_error("cannot open " + path);
+    if (s == Status::CannotRead) throw std::runtime_error("cannot read " + path);
+    return to_array(v, (int64_t)rows.size(), n);
+  }, py::arg("path"), py::arg("n"), py::arg("rows"), py::arg("nthreads") = 0,
+     "the given rows of an n x n matrix file (one rank's share), same accept set as read_matrix_file");
 }

@@ -203,7 +203,7 @@ void AsyncHostDevice::wait_mark(int s, const std::shared_ptr<void>& h) {
                                          " s for an event (missing collective on a peer, or a dependency cycle)");
   });
 }
-void AsyncHostDevice::occupy(int s, int, double us) {
+void AsyncHostDevice::occupy(int s, int, double us, int) {
   if (us > 0) enqueue(s, [us] { std::this_thread::sleep_for(std::chrono::duration<double, std::micro>(us)); });
 }
 

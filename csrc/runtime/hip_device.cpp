@@ -183,8 +183,8 @@ std::shared_ptr<void> HipDevice::mark(int s) {
 void HipDevice::wait_mark(int s, const std::shared_ptr<void>& h) {
   if (h) HIP_OK(hipStreamWaitEvent(hs(streams_[s]), static_cast<hipEvent_t>(h.get()), 0));
 }
-void HipDevice::occupy(int s, int nwg, double us) {
-  kern::spin(nwg, us, hs(streams_[s]));
+void HipDevice::occupy(int s, int nwg, double us, int lds_bytes) {
+  kern::spin(nwg, us, hs(streams_[s]), lds_bytes);
   check_launch();
 }
 

@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "gj/comms.hpp"
@@ -38,6 +40,14 @@ std::string RcclComm::unique_id() {
 RcclComm::RcclComm(const std::vector<std::string>& ids, int nranks, int rank, int device)
     : n_(nranks), r_(rank), device_(device) {
   GJ_REQUIRE(ids.size() == 2, "RcclComm needs two unique ids");
+  {
+    const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+    if (nranks > 1 && (!q || std::atoi(q) < kMinHwQueues))
+      std::fprintf(stderr,
+                   "gj: warning: GPU_MAX_HW_QUEUES=%s < %d; the SIDE and COMM communicators may share a "
+                   "hardware queue (set it before the first HIP call, see runtime_env.py)\n",
+                   q ? q : "unset", kMinHwQueues);
+  }
   (void)hipSetDevice(device_);
   for (int c = 0; c < 2; ++c) {
     GJ_REQUIRE(ids[c].size() == sizeof(ncclUniqueId), "bad unique id size");

@@ -1,4 +1,5 @@
 // ShadowComm: see gj/comms.hpp.
+#include <algorithm>
 #include <cstring>
 
 #include "gj/comms.hpp"
@@ -6,7 +7,29 @@
 
 namespace gj {
 
+std::string ShadowComm::describe() const {
+  std::string d = "shadow(" + std::to_string(p_);
+  if (cm_.bw_gbs > 0)
+    d += ", cost model " + std::to_string(cm_.bw_gbs) + " GB/s + " + std::to_string(cm_.lat_us) + " us on " +
+         std::to_string(cm_.channels) + " workgroups";
+  return d + ")";
+}
+
+void ShadowComm::cost(Device& dev, size_t bytes, int links, int s) {
+  if (!(cm_.bw_gbs > 0)) return;
+  const double us = cm_.lat_us + (double)bytes / (cm_.bw_gbs * 1e3 * std::max(1, links));
+  modelled_us_ += us;
+  dev.occupy(s, cm_.channels, us, cm_.lds_kib << 10);
+}
+
+void ShadowComm::group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) {
+  size_t out = 0, in = 0;  // the busier direction bounds the exchange
+  for (const auto& o : ops) (o.send ? out : in) += o.bytes;
+  if (!ops.empty()) cost(dev, std::max(out, in), std::min(p_ - 1, 7), s);
+}
+
 void ShadowComm::allgather(Device& dev, const void* send, void* recv, size_t bytes, int s) {
+  cost(dev, bytes * (p_ - 1), 1, s);
   dev.copy(recv, send, bytes, s);  // slot 0 = own contribution
   if (bytes != sizeof(PivotRec)) {  // residual/corner gathers: replicate rank 0
     for (int q = 1; q < p_; ++q) dev.copy(static_cast<char*>(recv) + q * bytes, send, bytes, s);
@@ -28,6 +51,7 @@ void ShadowComm::allgather(Device& dev, const void* send, void* recv, size_t byt
 }
 
 void ShadowComm::bcast(Device& dev, void* buf, size_t bytes, int root, int s) {
+  cost(dev, bytes, 1, s);
   if (root != 0) dev.memset0(buf, bytes, s);
 }
 

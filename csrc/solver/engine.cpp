@@ -21,6 +21,8 @@
 // Nothing cancels (no I + H tricks), so the numerics match the step-by-step reference.
 #include "gj/engine.hpp"
 
+#include "gj/io.hpp"
+
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
@@ -384,6 +386,42 @@ void Engine::download_rows_device(void* dst, int64_t ld) {
   if (real > 0)
     dev_.copy2d(dst, ld * esz(), out_, L_.npad * esz(), L_.n * esz(), real, S_MAIN);
   dev_.sync_stream(S_MAIN);
+}
+
+// One rank's share of a matrix file (reference read_matrix, main.cpp:209-282: there one rank parses
+// everything and sends every block row to its owner; here every rank maps the file and parses
+// only its own rows, so no rank holds more than its share).  Errors are agreed in the reference's
+// order: "cannot open" on any rank first, then "cannot read".
+Status Engine::read_file_rows(const std::string& path, int nthreads, std::vector<double>& rows) {
+  std::vector<int64_t> mine;
+  const int64_t real = real_local_rows();
+  mine.reserve((size_t)real);
+  for (int64_t r = 0; r < real; ++r) mine.push_back(L_.global_row(r));
+  Status s = Status::Ok;
+  try {
+    s = read_matrix_rows(path, L_.n, mine, rows, nthreads);
+  } catch (const std::bad_alloc&) {
+    s = Status::CannotRead;
+  }
+  if (comm_.host_max(dev_, s == Status::CannotOpen ? 1.0 : 0.0) > 0) return Status::CannotOpen;
+  if (comm_.host_max(dev_, s != Status::Ok ? 1.0 : 0.0) > 0) return Status::CannotRead;
+  return Status::Ok;
+}
+
+Status Engine::load_file(const std::string& path, int nthreads) {
+  std::vector<double> rows;
+  const Status s = read_file_rows(path, nthreads, rows);
+  if (s == Status::Ok) upload_local_rows(rows.data(), L_.n);
+  return s;
+}
+
+double Engine::residual_file(const std::string& path, int nthreads, Status* status) {
+  GJ_REQUIRE(solved_, "residual: solve() first");
+  std::vector<double> rows;
+  const Status s = read_file_rows(path, nthreads, rows);  // re-read, like main.cpp:463-484
+  if (status) *status = s;
+  if (s != Status::Ok) return -1.0;
+  return residual_rows(rows.data(), L_.n);
 }
 
 double Engine::norm_inf() {

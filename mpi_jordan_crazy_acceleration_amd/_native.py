@@ -9,7 +9,11 @@ from __future__ import annotations
 import importlib
 import os
 
-import torch  # noqa: F401  -- must be loaded before _C (shared libamdhip64 / librccl)
+from .runtime_env import configure_runtime_env
+
+configure_runtime_env()  # before anything initialises HIP (runtime_env.py)
+
+import torch  # noqa: E402,F401  -- must be loaded before _C (shared libamdhip64 / librccl)
 
 _C = None
 

@@ -16,7 +16,7 @@ import torch
 from .._native import load_native
 
 STATUS = {0: "ok", 1: "singular matrix", 2: "not enough memory", 3: "cannot open", 4: "cannot read",
-          5: "bad arguments", 6: "communication error"}
+          5: "bad arguments", 6: "communication error", 7: "not enough memory for block"}
 
 
 class SingularMatrixError(ArithmeticError):

@@ -83,6 +83,15 @@ class TorchDistComm:
         return float(t.item())
 
 
+def _raise_file_status(st: int, path, what: str = "") -> None:
+    if st == 3:
+        raise FileNotFoundError(f"cannot open{what} {path}")
+    if st == 4:
+        raise ValueError(f"cannot read{what} {path}")
+    if st != 0:
+        raise RuntimeError(f"unknown error {st} in {path}")
+
+
 class DistributedGaussJordan:
     """Block-row-cyclic Gauss-Jordan inversion with one rank per process.
 
@@ -132,6 +141,20 @@ class DistributedGaussJordan:
         """Load this rank's rows of the full matrix A (every rank may pass the full matrix)."""
         A = np.asarray(A, dtype=np.float64)
         self.engine.upload_local_rows(np.ascontiguousarray(A[self._rows]))
+
+    def load_file(self, path: str, nthreads: int = 0) -> None:
+        """Collective: every rank maps the file and parses only its own block rows (text in the
+        scanf("%lf") accept set, or raw fp64 ``.bin``), so no rank ever holds more than its share of
+        the matrix.  Raises ``FileNotFoundError("cannot open ...")`` / ``ValueError("cannot read
+        ...")`` on EVERY rank when any rank fails (reference read_matrix, main.cpp:209-282)."""
+        st = self.engine.load_file(str(path), int(nthreads))
+        _raise_file_status(st, path)
+
+    def residual_file(self, path: str, nthreads: int = 0) -> float:
+        """||A inv(A) - I||_inf with A re-read from the file (reference main.cpp:463-519)."""
+        st, res = self.engine.residual_file(str(path), int(nthreads))
+        _raise_file_status(st, path, " for residual")
+        return res
 
     def load_local_rows(self, rows: np.ndarray) -> None:
         self.engine.upload_local_rows(np.ascontiguousarray(rows, dtype=np.float64))

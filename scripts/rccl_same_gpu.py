@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--gen", default="random")
     ap.add_argument("--reps", type=int, default=2)
     args = ap.parse_args()
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    os.environ["GPU_MAX_HW_QUEUES"] = str(max(16, int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))))
     import torch.distributed as dist
     from mpi_jordan_crazy_acceleration_amd import load_native
 

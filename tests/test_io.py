@@ -33,3 +33,45 @@ def test_reader_parallel_large(native, tmp_path):
     assert f.stat().st_size > (1 << 20)
     B = native.read_matrix_file(str(f), n)
     assert np.array_equal(A, B)
+
+
+def test_reader_rows_subset(native, tmp_path):
+    # one rank's block rows (block-row-cyclic, m = 7, p = 3, rank 1), text and .bin, several threads
+    n, m, p, k = 300, 7, 3, 1
+    A = np.random.default_rng(1).standard_normal((n, n))
+    f = tmp_path / "a.txt"
+    np.savetxt(f, A, fmt="%.17g")
+    rows = [r for r in range(n) if (r // m) % p == k]
+    for nt in (1, 3, 8):
+        B = native.read_matrix_rows(str(f), n, rows, nt)
+        assert np.array_equal(B, A[rows])
+    g = tmp_path / "a.bin"
+    A.tofile(g)
+    assert np.array_equal(native.read_matrix_rows(str(g), n, rows), A[rows])
+    with pytest.raises(RuntimeError, match="cannot read"):
+        native.read_matrix_rows(str(g), n + 1, [0])
+
+
+@pytest.mark.parametrize("where", [0.3, 0.8])
+def test_reader_bad_token_late_chunk(native, tmp_path, where):
+    # > 1 MiB: chunked; an invalid token deep inside fails, an irregular glued pair ("1-2") before
+    # it shifts every later index (exact sequential fallback), rows of another rank skip the check
+    n = 400
+    A = np.random.default_rng(2).standard_normal((n, n))
+    toks = [f"{v:.17g}" for v in A.ravel()]
+    bad = int(where * len(toks))
+    toks_bad = list(toks)
+    toks_bad[bad] = "zz"
+    f = tmp_path / "bad.txt"
+    f.write_text(" ".join(toks_bad))
+    with pytest.raises(RuntimeError, match="cannot read"):
+        native.read_matrix_file(str(f), n)
+    r_bad = bad // n
+    other = [r for r in range(n) if r != r_bad][:50]
+    assert np.array_equal(native.read_matrix_rows(str(f), n, other), A[other])
+    # irregular: tokens i and i+1 glued as "a-b" (b negative) -> same numbers, sequential scan
+    i = next(j for j in range(bad // 2, len(toks) - 1) if toks[j + 1].startswith("-"))
+    toks_irr = toks[:i] + [toks[i] + toks[i + 1]] + toks[i + 2:]
+    g = tmp_path / "irr.txt"
+    g.write_text(" ".join(toks_irr))
+    assert np.array_equal(native.read_matrix_file(str(g), n), A)
