@@ -27,6 +27,8 @@
 //   --out FILE           write the inverse (text, or .bin)
 //   --rhs ones|random|FILE  also solve A x = b (x = inv(A) b) and report ||A x - b||_inf
 //   --out-x FILE         write x (text, or .bin); implies --rhs ones unless --rhs is given
+//   --refine K           at most K refinement steps of x with the residual in fp64 (default: 10 for
+//                        fp32 solves, 2 for fp64; Engine::solve_rhs)
 //   --json               machine-readable report on stderr
 //   --bcast auto|ring|direct  pivot-row broadcast algorithm at p > 2 (sets GJ_BCAST; auto = timed
 //                        against each other at startup, Comm::tune_bcast)
@@ -67,20 +69,29 @@ static void json_report(const RunConfig& cfg, const RunReport& rep) {
   }
   std::string rhs;
   if (rep.rhs_solved) {
-    char buf[128];
-    std::snprintf(buf, sizeof buf, ", \"axb_residual\": %.6e, \"axb_seconds\": %.6f", rep.rhs_residual,
-                  rep.rhs_seconds);
+    char buf[256];
+    std::snprintf(buf, sizeof buf,
+                  ", \"axb_residual\": %.6e, \"axb_seconds\": %.6f, \"axb_backward_error\": %.6e, "
+                  "\"refine_steps\": %d, \"refine_converged\": %s, \"axb_history\": [",
+                  rep.rhs_residual, rep.rhs_seconds, rep.rhs_backward_error, rep.rhs_steps,
+                  rep.rhs_converged ? "true" : "false");
     rhs = buf;
+    for (size_t i = 0; i < rep.rhs_history.size(); ++i) {
+      std::snprintf(buf, sizeof buf, "%s%.3e", i ? ", " : "", rep.rhs_history[i]);
+      rhs += buf;
+    }
+    rhs += "]";
   }
   std::fprintf(stderr,
                "{\"n\": %lld, \"m\": %lld, \"ranks\": %d, \"device\": \"%s\", \"comm\": \"%s\", "
                "\"dtype\": \"%s\", \"status\": %d, \"glob_time\": %.6f, \"best_time\": %.6f, "
                "\"gflops_nominal\": %.3f, \"residual\": %.6e, \"residual_computed\": %s, "
-               "\"host_wait_ms\": %.3f, \"offdiag_pivots\": %lld%s%s}\n",
+               "\"residual_fp64\": %s, \"host_wait_ms\": %.3f, \"offdiag_pivots\": %lld%s%s}\n",
                (long long)cfg.n, (long long)cfg.m, cfg.ranks, rep.device_desc.c_str(),
                rep.comm_desc.c_str(), dtype_name(cfg.solve.dtype), (int)rep.status, rep.glob_time,
                rep.best_time, rep.gflops_nominal, rep.residual,
-               rep.residual_computed ? "true" : "false", rep.stats.host_wait_ms,
+               rep.residual_computed ? "true" : "false", rep.residual_fp64 ? "true" : "false",
+               rep.stats.host_wait_ms,
                (long long)rep.stats.offdiag_pivots, phases.c_str(), rhs.c_str());
 }
 
@@ -139,6 +150,7 @@ int main(int argc, char* argv[]) {
       else if (a == "--out") out_file = val("--out");
       else if (a == "--rhs") cfg.rhs = val("--rhs");
       else if (a == "--out-x") x_file = val("--out-x");
+      else if (a == "--refine") cfg.refine = std::atoi(val("--refine"));
       else if (a == "--json") json = true;
       else if (a == "--bcast") {
         const std::string b = val("--bcast");

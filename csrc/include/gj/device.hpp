@@ -117,6 +117,9 @@ class Device {
   // X[r][c] := src[r][c] (doubles, ld src_ld) for r < rows, c < cols (dtype conversion).
   virtual void upload_convert(DType dt, void* X, int64_t ldx, const double* src_dev, int64_t src_ld,
                               int64_t rows, int64_t cols, int s) = 0;
+  // dst[r*ldd + c] := (double)X[r*ldx + c] for r < rows, c < cols (X of dtype dt, device memory).
+  virtual void widen(DType dt, double* dst, int64_t ldd, const void* X, int64_t ldx, int64_t rows,
+                     int64_t cols, int s) = 0;
   // Lt[c*ldl + r] = -X[r*ldx + col0 + c]  for r < rows, c < m   (multiplier panel, K-major).
   virtual void extract_neg_t(DType dt, void* Lt, int64_t ldl, const void* X, int64_t ldx,
                              int64_t rows, int64_t col0, int64_t m, int s) = 0;

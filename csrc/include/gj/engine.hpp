@@ -76,6 +76,15 @@ struct SolveStats {
   int64_t phase_calls[kNumPhases] = {};
 };
 
+// Result of Engine::solve_rhs.
+struct RhsResult {
+  double residual = 0;           // ||b - A x||_inf (fp64) of the returned x
+  double backward_error = 0;     // ||b - A x|| / (||A|| ||x|| + ||b||), inf-norms
+  std::vector<double> history;   // ||b - A x_k||_inf / ||b||_inf for k = 0 (x = X b), 1, ...
+  int steps = 0;                 // refinement steps applied
+  bool converged = false;        // backward error <= tol
+};
+
 class Engine {
  public:
   Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions& opt);
@@ -123,6 +132,13 @@ class Engine {
   void apply_inverse(const double* b, double* x);
   // ||A x - b||_inf with the input panel currently holding A (after generate/upload; collective).
   double axb_residual(const double* x, const double* b);
+  // A x = b with iterative refinement, the residual always in fp64 (A from `gen` or from this
+  // rank's fp64 rows `host_rows`, ld): x_0 = inv(A) b, x_{k+1} = x_k + inv(A) (b - A x_k).
+  // Collective; b and x are full n-vectors on every rank.
+  RhsResult solve_rhs(const double* b, double* x, const GenSpec* gen, const double* host_rows, int64_t ld,
+                      int max_refine, double tol);
+  // Precision of the last residual: true = fp64 (always for fp64 solves; fp32 solves when it fits).
+  bool residual_fp64() const { return last_residual_fp64_; }
 
   int64_t real_local_rows() const;
   int depth() const { return d_; }  // elimination steps per panel (after the auto choice)
@@ -143,7 +159,10 @@ class Engine {
   void chunk_pipeline(int64_t v, bool wait_main);
   void big_update(int64_t u);
   void finalize(const std::vector<int32_t>& seq);
-  double residual_common();
+  double residual_common(const void* A, bool wide);
+  bool residual_wide();
+  size_t residual_fp64_bytes() const;
+  void upload_rows_into(void* P, DType dt, const double* host, int64_t ld);
   Status read_file_rows(const std::string& path, int nthreads, std::vector<double>& rows);
   void dbg_sync();
   // Host wait for the pivot result of `step` (pinned slot par) with failure detection
@@ -228,6 +247,7 @@ class Engine {
   // The work space did not fit on some rank (agreed at construction): solve() reports
   // Status::NoBlockMemory, the reference's "not enough memory for block" (main.cpp:428-436).
   bool block_mem_fail_ = false;
+  bool last_residual_fp64_ = true;
   std::string block_mem_why_;
 };
 

@@ -47,6 +47,8 @@ class HipDevice : public Device {
   void occupy(int s, int nwg, double us, int lds_bytes = 0) override;
 
   void generate(DType dt, void* X, const Layout& L, GenSpec g, int s) override;
+  void widen(DType dt, double* dst, int64_t ldd, const void* X, int64_t ldx, int64_t rows, int64_t cols,
+             int s) override;
   void upload_convert(DType dt, void* X, int64_t ldx, const double* src_dev, int64_t src_ld,
                       int64_t rows, int64_t cols, int s) override;
   void extract_neg_t(DType dt, void* Lt, int64_t ldl, const void* X, int64_t ldx, int64_t rows,

@@ -34,6 +34,10 @@ struct RunConfig {
   std::string rhs;
   const double* rhs_input = nullptr;  // or a caller-owned n-vector
   bool keep_solution = false;         // return x in RunReport::x
+  // iterative refinement of x with the residual in fp64 (Engine::solve_rhs): at most `refine`
+  // steps (-1 = auto: 10 for fp32 solves, 2 for fp64), stop at backward error <= refine_tol
+  int refine = -1;
+  double refine_tol = 1e-15;
 };
 
 struct RunReport {
@@ -50,7 +54,12 @@ struct RunReport {
   std::string device_desc, comm_desc;
   double gflops_nominal = 0;        // 2 n^3 / glob_time / 1e9
   bool rhs_solved = false;
-  double rhs_residual = 0;          // ||A x - b||_inf
+  double rhs_residual = 0;          // ||A x - b||_inf (fp64)
+  std::vector<double> rhs_history;  // ||A x_k - b|| / ||b|| per refinement step (k = 0: x = inv(A) b)
+  int rhs_steps = 0;
+  bool rhs_converged = false;
+  double rhs_backward_error = 0;
+  bool residual_fp64 = true;        // precision of `residual` (fp32 solves: fp64 when it fits)
   double rhs_seconds = 0;           // x = inv(A) b (GEMV + all-gather), max over ranks
   std::vector<double> x_head;       // first min(n, print_max) entries of x
   std::vector<double> x;            // n entries if keep_solution

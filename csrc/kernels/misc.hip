@@ -82,6 +82,29 @@ void upload_convert(DType dt, void* X, int64_t ldx, const double* src, int64_t s
                        src, src_ld, rows, cols);
 }
 
+// dst[r*ldd + j] = (double)X[r*ldx + j]  (fp64 residual / refinement of an fp32 solve)
+template <typename T>
+__global__ void widen_kernel(double* dst, int64_t ldd, const T* X, int64_t ldx, int64_t rows, int64_t cols) {
+  const int64_t total = rows * cols;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / cols, j = e - r * cols;
+    dst[r * ldd + j] = (double)X[r * ldx + j];
+  }
+}
+
+void widen(DType dt, double* dst, int64_t ldd, const void* X, int64_t ldx, int64_t rows, int64_t cols,
+           hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return;
+  const unsigned grid = grid_for(rows * cols, 256 * 4);
+  if (dt == DType::F64)
+    hipLaunchKernelGGL(widen_kernel<double>, dim3(grid), dim3(256), 0, s, dst, ldd,
+                       static_cast<const double*>(X), ldx, rows, cols);
+  else
+    hipLaunchKernelGGL(widen_kernel<float>, dim3(grid), dim3(256), 0, s, dst, ldd,
+                       static_cast<const float*>(X), ldx, rows, cols);
+}
+
 // ---------------------------------------------------------------- extract_neg_t (tiled transpose)
 template <typename T>
 __global__ __launch_bounds__(256) void extract_kernel(T* __restrict__ Lt, int64_t ldl,

@@ -499,6 +499,8 @@ PYBIND11_MODULE(_C, mod) {
     if (d.contains("keep_inverse")) c.keep_inverse = d["keep_inverse"].cast<bool>();
     if (d.contains("host_threads")) c.host_threads = d["host_threads"].cast<int>();
     if (d.contains("repeats")) c.repeats = d["repeats"].cast<int>();
+    if (d.contains("refine")) c.refine = d["refine"].cast<int>();
+    if (d.contains("refine_tol")) c.refine_tol = d["refine_tol"].cast<double>();
     py::array_t<double, py::array::c_style | py::array::forcecast> inp;
     if (d.contains("input") && !d["input"].is_none()) {
       inp = d["input"].cast<py::array_t<double, py::array::c_style | py::array::forcecast>>();
@@ -524,6 +526,7 @@ PYBIND11_MODULE(_C, mod) {
     o["best_time"] = r.best_time;
     o["residual_computed"] = r.residual_computed;
     o["residual"] = r.residual;
+    o["residual_fp64"] = r.residual_fp64;
     o["nm"] = r.nm;
     o["corner_a"] = to_array(r.corner_a, r.corner_a.empty() ? 0 : r.nm, r.corner_a.empty() ? 0 : r.nm);
     o["corner_inv"] = to_array(r.corner_inv, r.corner_inv.empty() ? 0 : r.nm, r.corner_inv.empty() ? 0 : r.nm);
@@ -535,6 +538,10 @@ PYBIND11_MODULE(_C, mod) {
     if (r.rhs_solved) {
       o["axb_residual"] = r.rhs_residual;
       o["axb_seconds"] = r.rhs_seconds;
+      o["axb_history"] = r.rhs_history;
+      o["refine_steps"] = r.rhs_steps;
+      o["refine_converged"] = r.rhs_converged;
+      o["axb_backward_error"] = r.rhs_backward_error;
       o["x_head"] = r.x_head;
       if (c.keep_solution) o["x"] = to_array(r.x, c.n, 1);
     }

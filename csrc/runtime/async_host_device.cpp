@@ -211,6 +211,10 @@ void AsyncHostDevice::occupy(int s, int, double us, int) {
 void AsyncHostDevice::generate(DType dt, void* X, const Layout& L, GenSpec g, int s) {
   enqueue(s, [=] { inner_.generate(dt, X, L, g, s); });
 }
+void AsyncHostDevice::widen(DType dt, double* dst, int64_t ldd, const void* X, int64_t ldx, int64_t rows,
+                            int64_t cols, int s) {
+  enqueue(s, [=] { inner_.widen(dt, dst, ldd, X, ldx, rows, cols, s); });
+}
 void AsyncHostDevice::upload_convert(DType dt, void* X, int64_t ldx, const double* src, int64_t src_ld,
                                      int64_t rows, int64_t cols, int s) {
   enqueue(s, [=] { inner_.upload_convert(dt, X, ldx, src, src_ld, rows, cols, s); });

@@ -209,6 +209,11 @@ void HipDevice::generate(DType dt, void* X, const Layout& L, GenSpec g, int s) {
   kern::generate(dt, X, L, (int)g.kind, g.seed, hs(streams_[s]));
   check_launch();
 }
+void HipDevice::widen(DType dt, double* dst, int64_t ldd, const void* X, int64_t ldx, int64_t rows,
+                      int64_t cols, int s) {
+  kern::widen(dt, dst, ldd, X, ldx, rows, cols, hs(streams_[s]));
+  check_launch();
+}
 void HipDevice::upload_convert(DType dt, void* X, int64_t ldx, const double* src, int64_t src_ld,
                                int64_t rows, int64_t cols, int s) {
   kern::upload_convert(dt, X, ldx, src, src_ld, rows, cols, hs(streams_[s]));

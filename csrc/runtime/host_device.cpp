@@ -159,6 +159,13 @@ void HostDevice::generate(DType dt, void* X, const Layout& L, GenSpec g, int) {
   });
 }
 
+void HostDevice::widen(DType dt, double* dst, int64_t ldd, const void* X, int64_t ldx, int64_t rows,
+                       int64_t cols, int) {
+  for (int64_t r = 0; r < rows; ++r)
+    for (int64_t j = 0; j < cols; ++j)
+      dst[r * ldd + j] = dt == DType::F64 ? tp<double>(X)[r * ldx + j] : (double)tp<float>(X)[r * ldx + j];
+}
+
 void HostDevice::upload_convert(DType dt, void* X, int64_t ldx, const double* src, int64_t src_ld,
                                 int64_t rows, int64_t cols, int) {
   for (int64_t r = 0; r < rows; ++r)

@@ -348,25 +348,7 @@ void Engine::generate(GenSpec g) {
 }
 
 void Engine::upload_local_rows(const double* host, int64_t ld) {
-  GenSpec z;
-  z.kind = GenKind::Zero;  // zero + identity on the padded diagonal
-  dev_.generate(opt_.dtype, X_, L_, z, S_MAIN);
-  const int64_t real = real_local_rows();
-  const int64_t n = L_.n;
-  if (real > 0) {
-    // stream the rows through a bounded staging buffer (<= 256 MiB)
-    const int64_t rows_per = std::max<int64_t>(1, (int64_t(256) << 20) / (n * 8));
-    const int64_t chunk = std::min(rows_per, real);
-    double* stage = static_cast<double*>(dev_.alloc(sizeof(double) * chunk * n));
-    for (int64_t r0 = 0; r0 < real; r0 += chunk) {
-      const int64_t nr = std::min(chunk, real - r0);
-      dev_.copy2d(stage, n * 8, host + r0 * ld, ld * 8, n * 8, nr, S_MAIN);
-      dev_.upload_convert(opt_.dtype, elem(X_, r0 * L_.npad), L_.npad, stage, n, nr, n, S_MAIN);
-      dev_.sync_stream(S_MAIN);
-    }
-    dev_.release(stage);
-  }
-  dev_.sync_stream(S_MAIN);
+  upload_rows_into(X_, opt_.dtype, host, ld);
   solved_ = false;
 }
 
@@ -886,7 +868,27 @@ std::vector<double> Engine::corner(int nm, int which) {
   return res;
 }
 
-double Engine::residual_common() {
+// Bytes the fp64 check of an fp32 solve needs on this rank beyond the solve's own buffers: the
+// fp64 copy of A's rows, the widened inverse and, at p > 1, the gathered fp32 inverse.
+size_t Engine::residual_fp64_bytes() const {
+  const size_t npad = (size_t)L_.npad, rows = (size_t)std::max<int64_t>(L_.rows, 1);
+  size_t b = rows * npad * 8 + npad * npad * 8;
+  if (L_.p > 1) b += npad * npad * esz() + (size_t)L_.max_nblk * L_.m * npad * esz() * (L_.p + 1);
+  return b;
+}
+
+// Collective: the residual of an fp32 solve is computed in fp64 (fp64 A, widened inverse, fp64
+// MFMA accumulation: the reference's check, main.cpp:490-507, is fp64) whenever that fits on every
+// rank; otherwise in fp32 against the fp32 matrix (residual_precision() says which).
+bool Engine::residual_wide() {
+  if (opt_.dtype == DType::F64) return false;
+  const bool fits = !injected_alloc_fail(L_.k, "residual64") &&
+                    (!dev_.on_gpu() || residual_fp64_bytes() + (64u << 20) <= dev_.free_memory());
+  return comm_.host_max(dev_, fits ? 0.0 : 1.0) == 0.0;
+}
+
+// A: this rank's rows of the matrix (ld npad), fp64 when wide, else the engine dtype.
+double Engine::residual_common(const void* A, bool wide) {
   const int64_t m = L_.m, p = L_.p, npad = L_.npad;
   const size_t es = esz();
   void* full = out_;
@@ -922,29 +924,87 @@ double Engine::residual_common() {
     if (tmp) dev_.release(tmp);
     dev_.release(gath);
   }
+  const DType rdt = wide ? DType::F64 : opt_.dtype;
+  void* fullr = full;
+  if (rdt != opt_.dtype) {  // widen the inverse (fp32 -> fp64)
+    fullr = dev_.alloc((size_t)npad * npad * 8);
+    dev_.widen(opt_.dtype, static_cast<double*>(fullr), npad, full, npad, npad, npad, S_MAIN);
+  }
   double local = 0.0;
   if (L_.nblk > 0) {
-    dev_.residual(opt_.dtype, X_, full, L_, dscratch_, S_MAIN);
+    dev_.residual(rdt, A, fullr, L_, dscratch_, S_MAIN);
     dev_.copy(dhost_, dscratch_, sizeof(double), S_MAIN);
     dev_.sync_stream(S_MAIN);
     local = dhost_[0];
   }
+  dev_.sync_stream(S_MAIN);
+  if (fullr != full) dev_.release(fullr);
   if (p > 1) dev_.release(full);
+  last_residual_fp64_ = (rdt == DType::F64);
   return comm_.host_max(dev_, local);
 }
 
 double Engine::residual_generated(GenSpec g) {
   GJ_REQUIRE(solved_, "residual: solve() first");
+  if (residual_wide()) {  // fp64 A straight from the generator
+    void* Aw = dev_.alloc((size_t)std::max<int64_t>(L_.rows, 1) * L_.npad * 8);
+    dev_.generate(DType::F64, Aw, L_, g, S_MAIN);
+    double r = 0;
+    try {
+      r = residual_common(Aw, true);
+    } catch (...) {
+      dev_.release(Aw);
+      throw;
+    }
+    dev_.release(Aw);
+    return r;
+  }
   dev_.generate(opt_.dtype, X_, L_, g, S_MAIN);
   dev_.sync_stream(S_MAIN);
-  return residual_common();
+  return residual_common(X_, false);
+}
+
+// this rank's real rows from host doubles into panel P (dtype dt, ld npad): zero + identity padding,
+// then through a bounded staging buffer (<= 256 MiB)
+void Engine::upload_rows_into(void* P, DType dt, const double* host, int64_t ld) {
+  GenSpec z;
+  z.kind = GenKind::Zero;
+  dev_.generate(dt, P, L_, z, S_MAIN);
+  const int64_t real = real_local_rows(), n = L_.n;
+  if (real > 0) {
+    const int64_t rows_per = std::max<int64_t>(1, (int64_t(256) << 20) / (n * 8));
+    const int64_t chunk = std::min(rows_per, real);
+    double* stage = static_cast<double*>(dev_.alloc(sizeof(double) * chunk * n));
+    for (int64_t r0 = 0; r0 < real; r0 += chunk) {
+      const int64_t nr = std::min(chunk, real - r0);
+      dev_.copy2d(stage, n * 8, host + r0 * ld, ld * 8, n * 8, nr, S_MAIN);
+      dev_.upload_convert(dt, static_cast<char*>(P) + (size_t)r0 * L_.npad * dtype_size(dt), L_.npad, stage, n,
+                          nr, n, S_MAIN);
+      dev_.sync_stream(S_MAIN);
+    }
+    dev_.release(stage);
+  }
+  dev_.sync_stream(S_MAIN);
 }
 
 double Engine::residual_rows(const double* host, int64_t ld) {
   GJ_REQUIRE(solved_, "residual: solve() first");
+  if (residual_wide()) {
+    void* Aw = dev_.alloc((size_t)std::max<int64_t>(L_.rows, 1) * L_.npad * 8);
+    double r = 0;
+    try {
+      upload_rows_into(Aw, DType::F64, host, ld);
+      r = residual_common(Aw, true);
+    } catch (...) {
+      dev_.release(Aw);
+      throw;
+    }
+    dev_.release(Aw);
+    return r;
+  }
   upload_local_rows(host, ld);
   solved_ = true;
-  return residual_common();
+  return residual_common(X_, false);
 }
 
 // ---------------------------------------------------------------- A x = b
@@ -1008,6 +1068,82 @@ double Engine::axb_residual(const double* x, const double* b) {
     if (gi < n) local = std::max(local, std::fabs(y[i] - b[gi]));
   }
   return comm_.host_max(dev_, local);
+}
+
+// x = inv(A) b, then iterative refinement with the residual in fp64:
+//   r_k = b - A x_k  (A in fp64: regenerated, or re-uploaded from the caller's fp64 rows;
+//                     fp64 MFMA GEMV, the full vector all-gathered)
+//   x_{k+1} = x_k + X r_k   (X = the computed inverse, engine dtype)
+// It converges when ||I - X A|| < 1; each step gains about -log10 ||I - X A|| digits.  Stops at
+// the normwise backward error ||r|| / (||A|| ||x|| + ||b||) <= tol (inf-norms), after max_refine
+// steps, or when the residual stops shrinking
+// (refinement cannot converge: reported, not hidden).
+RhsResult Engine::solve_rhs(const double* b, double* x, const GenSpec* gen, const double* host_rows,
+                            int64_t ld, int max_refine, double tol) {
+  GJ_REQUIRE(solved_, "solve_rhs: solve() first");
+  GJ_REQUIRE(gen || host_rows || real_local_rows() == 0,
+             "solve_rhs: the matrix (generator or rows) is needed for the fp64 residual");
+  const int64_t m = L_.m, n = L_.n;
+  RhsResult rr;
+  void* Aw = dev_.alloc((size_t)std::max<int64_t>(L_.rows, 1) * L_.npad * 8);
+  try {
+    if (gen) dev_.generate(DType::F64, Aw, L_, *gen, S_MAIN);
+    else upload_rows_into(Aw, DType::F64, host_rows, ld);
+    dev_.sync_stream(S_MAIN);
+    double bn = 0;
+    for (int64_t i = 0; i < n; ++i) bn = std::max(bn, std::fabs(b[i]));
+    if (bn == 0) bn = 1;
+    dev_.row_abs_max(DType::F64, Aw, L_.npad, L_, dscratch_, S_MAIN);  // ||A||_inf (fp64)
+    dev_.copy(dhost_, dscratch_, sizeof(double), S_MAIN);
+    dev_.sync_stream(S_MAIN);
+    const double an = comm_.host_max(dev_, L_.nblk > 0 ? dhost_[0] : 0.0);
+    apply_inverse(b, x);
+    std::vector<double> r((size_t)n), d((size_t)n);
+    double prev = 1e300;
+    for (int it = 0;; ++it) {
+      // r = b - A x (this rank's rows, fp64), all-gathered to the full vector
+      void* xd = upload_vector(dev_, DType::F64, x, n, L_.npad);
+      std::vector<double> y = local_matvec(dev_, DType::F64, Aw, L_, xd);
+      dev_.release(xd);
+      const int64_t per = L_.max_nblk * m;
+      std::vector<double> mine((size_t)per, 0.0), all((size_t)per * L_.p);
+      for (int64_t i = 0; i < L_.rows; ++i) {
+        const int64_t gi = L_.global_block(i / m) * m + i % m;
+        if (gi < n) mine[(size_t)i] = b[gi] - y[(size_t)i];
+      }
+      comm_.host_allgather(dev_, mine.data(), all.data(), sizeof(double) * per);
+      double rn = 0;
+      for (int64_t q = 0; q < L_.p; ++q)
+        for (int64_t j = 0; j < rows_owned(L_.Nr, L_.p, q); ++j)
+          for (int64_t e = 0; e < m; ++e) {
+            const int64_t gi = (j * L_.p + q) * m + e;
+            if (gi < n) {
+              r[(size_t)gi] = all[(size_t)q * per + j * m + e];
+              rn = std::max(rn, std::fabs(r[(size_t)gi]));
+            }
+          }
+      double xn = 0;
+      for (int64_t i = 0; i < n; ++i) xn = std::max(xn, std::fabs(x[i]));
+      rr.history.push_back(rn / bn);
+      rr.residual = rn;
+      rr.backward_error = rn / (an * xn + bn);
+      if (rr.backward_error <= tol) {
+        rr.converged = true;
+        break;
+      }
+      if (it >= max_refine) break;
+      if (it > 0 && rn > 0.5 * prev) break;  // not contracting: refinement cannot converge here
+      prev = rn;
+      apply_inverse(r.data(), d.data());
+      for (int64_t i = 0; i < n; ++i) x[i] += d[(size_t)i];
+      rr.steps = it + 1;
+    }
+  } catch (...) {
+    dev_.release(Aw);
+    throw;
+  }
+  dev_.release(Aw);
+  return rr;
 }
 
 void SelfComm::host_allgather(Device&, const void* send, void* recv, size_t bytes) {

@@ -164,15 +164,20 @@ void rank_main(const RunConfig& cfg, int rank, Shared& sh, std::shared_ptr<Loopb
     std::vector<double> x((size_t)cfg.n);
     comm->barrier(*dev);
     const auto t0 = std::chrono::steady_clock::now();
-    eng->apply_inverse(sh.b.data(), x.data());
+    const int refine = cfg.refine >= 0 ? cfg.refine : (cfg.solve.dtype == DType::F32 ? 10 : 2);
+    if (src && local.empty()) load();  // the fp64 rows of A (residual_rows keeps them in `local`)
+    const RhsResult rr = eng->solve_rhs(sh.b.data(), x.data(), src ? nullptr : &cfg.gen,
+                                        src ? local.data() : nullptr, cfg.n, refine, cfg.refine_tol);
     const double tx = comm->host_max(
         *dev, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
-    if (!do_res) load();  // the residual pass already put A back into the input panel
-    const double rr = eng->axb_residual(x.data(), sh.b.data());
     if (rank == 0) {
       std::lock_guard<std::mutex> lk(sh.mu);
       sh.rep.rhs_solved = true;
-      sh.rep.rhs_residual = rr;
+      sh.rep.rhs_residual = rr.residual;
+      sh.rep.rhs_history = rr.history;
+      sh.rep.rhs_steps = rr.steps;
+      sh.rep.rhs_converged = rr.converged;
+      sh.rep.rhs_backward_error = rr.backward_error;
       sh.rep.rhs_seconds = tx;
       sh.rep.x_head.assign(x.begin(), x.begin() + nm);
       if (cfg.keep_solution) sh.rep.x = x;
@@ -185,6 +190,7 @@ void rank_main(const RunConfig& cfg, int rank, Shared& sh, std::shared_ptr<Loopb
     sh.rep.best_time = best;
     sh.rep.residual_computed = do_res;
     sh.rep.residual = res;
+    sh.rep.residual_fp64 = eng->residual_fp64();
     sh.rep.nm = nm;
     const double n = (double)cfg.n;
     sh.rep.gflops_nominal = glob > 0 ? 2.0 * n * n * n / glob / 1e9 : 0.0;

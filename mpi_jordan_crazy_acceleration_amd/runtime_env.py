@@ -28,7 +28,7 @@ def configure_runtime_env(environ=None) -> dict:
         cur = int(env.get("GPU_MAX_HW_QUEUES", "4"))
     except ValueError:
         cur = 4
-    if cur < MIN_HW_QUEUES:
+    if cur < MIN_HW_QUEUES and env.get("GJ_KEEP_HW_QUEUES", "0") != "1":  # (A/B measurements only)
         env["GPU_MAX_HW_QUEUES"] = str(MIN_HW_QUEUES)
     env.setdefault("HIP_FORCE_DEV_KERNARG", "1")
     return {"GPU_MAX_HW_QUEUES": env["GPU_MAX_HW_QUEUES"], "HIP_FORCE_DEV_KERNARG": env["HIP_FORCE_DEV_KERNARG"]}
