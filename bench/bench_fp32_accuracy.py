@@ -24,30 +24,32 @@ def main():
     ap.add_argument("--block", type=int, default=128)
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--no-distance", action="store_true")
+    ap.add_argument("--gens", nargs="+", default=["random", "randshift"],
+                    help="random: uniform[-1,1) (kappa ~ 1e7-1e9 at these n); randshift: + sqrt(n) I (well conditioned)")
     args = ap.parse_args()
     from mpi_jordan_crazy_acceleration_amd import GaussJordan, load_native
     import torch
 
     C = load_native()
-    for n in args.sizes:
-        out = {"n": n, "m": args.block}
+    for n, gen in [(n, g) for n in args.sizes for g in args.gens]:
+        out = {"n": n, "m": args.block, "gen": gen}
         for dt in ("fp32", "fp64"):
             t0 = time.perf_counter()
             r = GaussJordan(block_size=args.block, device="gpu", dtype=dt).run(
-                n, gen="random", seed=args.seed, rhs="ones")
+                n, gen=gen, seed=args.seed, rhs="ones")
             out[dt] = {"status": r["status"], "solve_s": round(r["glob_time"], 4),
                        "residual": r["residual"], "residual_fp64": r["residual_fp64"],
                        "axb_history": r["axb_history"], "refine_converged": r["refine_converged"],
                        "axb_backward_error": r["axb_backward_error"],
                        "wall_s": round(time.perf_counter() - t0, 1)}
-            print(json.dumps({"n": n, dt: out[dt]}), flush=True)
+            print(json.dumps({"n": n, "gen": gen, dt: out[dt]}), flush=True)
         if not args.no_distance:
             dev = C.hip_device(0)
             comm = C.self_comm()
             inv = {}
             for dt, tdt in (("fp64", torch.float64), ("fp32", torch.float32)):
                 eng = C.Engine(dev, comm, n, args.block, dt)
-                eng.generate("random", args.seed)
+                eng.generate(gen, args.seed)
                 st = eng.solve()
                 assert st["status"] == 0
                 t = torch.empty((n, n), dtype=tdt, device="cuda")
@@ -61,7 +63,8 @@ def main():
                 d = inv["fp32"][r0:r0 + 4096].double() - x64[r0:r0 + 4096]
                 num = max(num, d.abs().sum(dim=1).max().item())
             out["inv_distance_rel"] = num / den
-            print(json.dumps({"n": n, "inv_distance_rel": out["inv_distance_rel"], "inv64_norm": den}), flush=True)
+            print(json.dumps({"n": n, "gen": gen, "inv_distance_rel": out["inv_distance_rel"], "inv64_norm": den}),
+                  flush=True)
             del inv, x64
             torch.cuda.empty_cache()
 

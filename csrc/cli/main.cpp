@@ -15,7 +15,7 @@
 //   --device gpu|cpu     execution backend (default: gpu when a HIP device exists)
 //   --comm auto|rccl|loopback|async   (async: stream-ordered virtual ranks; --jitter US)
 //   --dtype fp64|fp32
-//   --gen absdiff|hilbert|random|identity   generator when no file is given (reference: absdiff;
+//   --gen absdiff|hilbert|random|randshift|identity   generator when no file is given (reference: absdiff;
 //                        -DHILBERT -> --gen hilbert)
 //   --seed S             seed of --gen random
 //   --residual always|compat|never   compat = the reference's "p == 1!" skip (main.cpp:499-513)
@@ -134,6 +134,7 @@ int main(int argc, char* argv[]) {
         else if (g == "hilbert") cfg.gen.kind = GenKind::Hilbert;
         else if (g == "random") cfg.gen.kind = GenKind::Random;
         else if (g == "identity") cfg.gen.kind = GenKind::Identity;
+        else if (g == "randshift") cfg.gen.kind = GenKind::RandomShifted;
         else return usage(argv[0]);
       } else if (a == "--seed") cfg.gen.seed = std::strtoull(val("--seed"), nullptr, 10);
       else if (a == "--residual") {

@@ -21,7 +21,9 @@ namespace gj {
 
 // Matrix generators (reference f / f_i, main.cpp:47-64, plus a seeded random dense generator for
 // the synthetic benchmark system).
-enum class GenKind : int { AbsDiff = 0, Hilbert = 1, Identity = 2, Random = 3, Zero = 4 };
+// RandomShifted: Random + sqrt(n) on the diagonal (well conditioned at any n: where fp32 solves
+// and their refinement are meaningful, BASELINE.md "fp32").
+enum class GenKind : int { AbsDiff = 0, Hilbert = 1, Identity = 2, Random = 3, Zero = 4, RandomShifted = 5 };
 
 struct GenSpec {
   GenKind kind = GenKind::AbsDiff;

@@ -5,6 +5,8 @@
 // can produce any element without communication — the synthetic dense system of the benchmark.
 #pragma once
 
+#include <cmath>
+
 #include "gj/common.hpp"
 #include "gj/device.hpp"
 
@@ -29,9 +31,11 @@ GJ_HD inline double gen_value(int kind, uint64_t seed, int64_t n, int64_t i, int
       return 1.0 / (double)(i + j + 1);
     case 2:  // Identity
       return (i == j) ? 1.0 : 0.0;
-    case 3: {  // Random uniform [-1, 1)
+    case 3:    // Random uniform [-1, 1)
+    case 5: {  // RandomShifted: + sqrt(n) on the diagonal
       const uint64_t h = splitmix64(seed * 0x2545F4914F6CDD1Dull ^ ((uint64_t)i << 32) ^ (uint64_t)j);
-      return (double)(h >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+      const double u = (double)(h >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+      return (kind == 5 && i == j) ? u + sqrt((double)n) : u;
     }
     default:  // Zero
       return 0.0;

@@ -37,6 +37,7 @@ GenKind parse_gen(const std::string& s) {
   if (s == "hilbert") return GenKind::Hilbert;
   if (s == "identity") return GenKind::Identity;
   if (s == "random") return GenKind::Random;
+  if (s == "randshift") return GenKind::RandomShifted;
   if (s == "zero") return GenKind::Zero;
   throw std::invalid_argument("unknown generator " + s);
 }

@@ -50,7 +50,7 @@ def main(argv=None) -> int:
     ap.add_argument("pos", nargs="*")
     ap.add_argument("--device", choices=["auto", "gpu", "cpu"], default="auto")
     ap.add_argument("--dtype", choices=["fp64", "fp32"], default="fp64")
-    ap.add_argument("--gen", choices=["absdiff", "hilbert", "random", "identity"], default="absdiff")
+    ap.add_argument("--gen", choices=["absdiff", "hilbert", "random", "randshift", "identity"], default="absdiff")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--residual", choices=["always", "compat", "never"], default="always")
     ap.add_argument("--print-max", type=int, default=10)

@@ -30,6 +30,8 @@ def generate_matrix(n: int, kind: str = "absdiff", seed: int = 0) -> np.ndarray:
         return 1.0 / (i + j + 1).astype(np.float64)
     if kind == "identity":
         return np.eye(n)
+    if kind == "randshift":  # random + sqrt(n) I (gen.hpp GenKind::RandomShifted)
+        return generate_matrix(n, "random", seed) + np.sqrt(float(n)) * np.eye(n)
     if kind == "random":
         with np.errstate(over="ignore"):
             s = (np.uint64(seed) * np.uint64(0x2545F4914F6CDD1D)) & np.uint64(_MASK)
