@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Latency of the batched candidate-block inversion (pivot search) in isolation (device-side events).
 
-    python bench/bench_blockinv.py [panel] [panel_rl] [panel1] [sweep]
+    [BI_M="64 128"] [BI_NBLK="8 32 64 256"] python bench/bench_blockinv.py [panel] [panel_rl] [panel1] [sweep]
 """
 import json
 import os
@@ -17,8 +17,8 @@ def main(variants):
     C = load_native()
     for var in variants:
         C.set_block_inverse_variant(var)
-        for m in (64, 128):
-            for nblk in (8, 32, 64, 256):
+        for m in [int(x) for x in os.environ.get("BI_M", "64 128").split()]:
+            for nblk in [int(x) for x in os.environ.get("BI_NBLK", "8 32 64 256").split()]:
                 for dt in (torch.float64, torch.float32):
                     Lt = torch.randn(m, nblk * m, dtype=dt, device="cuda")
                     n = nblk * m

@@ -666,6 +666,9 @@ static void launch_bi(const void* Lt, int64_t ldl, void* inv_t, double* scores, 
       block_inverse_mfma(sizeof(T) == 8 ? DType::F64 : DType::F32, Lt, ldl, inv_t, scores, valid, used,
                          L, thresh, s, g_bi_variant == 0 ? 2 : g_bi_variant == 4 ? 1 : 0))
     return;
+  if (g_bi_variant != 1 && block_inverse_big(sizeof(T) == 8 ? DType::F64 : DType::F32, Lt, ldl, inv_t, scores,
+                                              valid, used, L, thresh, s, scratch))
+    return;
   if (g_bi_variant == 2 && m > 32 && m <= 64)
     hipLaunchKernelGGL((block_inverse_panel_kernel<T, 64, 256>), dim3(grid), dim3(256), 0, s, lt, ldl,
                        it, scores, valid, used, m, L.p, L.k, thresh);
@@ -693,6 +696,7 @@ static bool generic_path(DType dt, int64_t m) { return dt == DType::F64 ? m > 12
 
 size_t block_inverse_scratch_bytes(DType dt, const Layout& L) {
   if (!generic_path(dt, L.m)) return 0;
+  if (const size_t big = block_inverse_big_scratch_bytes(dt, L)) return big;
   return (size_t)L.nblk * L.m * L.m * dtype_size(dt);
 }
 size_t block_inverse_iscratch_bytes(const Layout& L) {

@@ -37,7 +37,15 @@ void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* s
 bool block_inverse_mfma(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                         int32_t* valid, const int32_t* used, const Layout& L, double thresh,
                         hipStream_t s, int pivot_variant /*0 LDS, 1 readlane, 2 pipelined*/);
-// scratch needed by the generic (m > 256) path
+// test probe: when set, the matrix-core block inverses write the pivot row of every column of
+// every candidate to piv_out[b * m + c] (device memory; nullptr = off)
+void set_block_inverse_probe(int32_t* piv_out);
+int32_t* block_inverse_probe();
+// blockinv_big.hip: fp64 128 < m <= 256 (false = not handled); scratch: nblk 256 x 256 images
+bool block_inverse_big(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,
+                       const int32_t* used, const Layout& L, double thresh, hipStream_t s, void* scratch);
+size_t block_inverse_big_scratch_bytes(DType dt, const Layout& L);
+// scratch needed by the fp64 m > 128 paths (big kernel / generic sweep)
 size_t block_inverse_scratch_bytes(DType dt, const Layout& L);
 size_t block_inverse_iscratch_bytes(const Layout& L);
 

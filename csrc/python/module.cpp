@@ -155,6 +155,8 @@ PYBIND11_MODULE(_C, mod) {
     else if (v == "panel_rl") kern::set_block_inverse_variant(4);
     else throw std::invalid_argument("block inverse variant: panel | sweep | panel1 | panel_lds | panel_rl");
   });
+  mod.def("set_block_inverse_probe", [](uintptr_t p) { kern::set_block_inverse_probe(reinterpret_cast<int32_t*>(p)); },
+          "test probe: device int32 buffer (nblk x m) receiving each candidate's pivot row per column; 0 = off");
   mod.def("set_gemm_variant", [](const std::string& v) { kern::set_gemm_variant(kern::gemm_variant_id(v.c_str())); });
 
   // Kernel-level entry points (raw pointers; used by the per-kernel numerics tests and
@@ -223,6 +225,22 @@ PYBIND11_MODULE(_C, mod) {
                  U used, int64_t n, int64_t m, int64_t p, int64_t k, double thresh) {
              d.block_inverse(parse_dtype(dt), (const void*)Lt, ldl, (void*)inv_t, (double*)scores,
                              (int32_t*)valid, (const int32_t*)used, lay(n, m, p, k), thresh, S_MAIN);
+             d.sync_stream(S_MAIN);
+           })
+      // pivot selection kernels (tests): local argmin of one rank's candidates -> 32-B record at rec
+      .def("pivot_local",
+           [lay](Device& d, U scores, U valid, U used, U pos, int64_t n, int64_t m, int64_t p, int64_t k, U rec) {
+             d.pivot_local((const double*)scores, (const int32_t*)valid, (const int32_t*)used,
+                           (const int32_t*)pos, lay(n, m, p, k), (PivotRec*)rec, S_MAIN);
+             d.sync_stream(S_MAIN);
+           })
+      // one rank: argmin + book-keeping (pos / phys_at / used / seq) + result record, one launch
+      .def("pivot_select_single",
+           [lay](Device& d, U scores, U valid, int64_t n, int64_t m, int t, U pos, U phys_at, U used, U seq,
+                 U rec, U out) {
+             d.pivot_select_single((const double*)scores, (const int32_t*)valid, lay(n, m, 1, 0), (int32_t)t,
+                                   (int32_t*)pos, (int32_t*)phys_at, (int32_t*)used, (int32_t*)seq,
+                                   (PivotRec*)rec, (PivotResult*)out, nullptr, S_MAIN);
              d.sync_stream(S_MAIN);
            })
       // Device-side latency of the batched block inverse: `reps` back-to-back launches on one

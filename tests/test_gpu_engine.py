@@ -9,7 +9,8 @@ from mpi_jordan_crazy_acceleration_amd.utils import gauss_jordan_reference, gene
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("n,m", [(1000, 128), (517, 60), (64, 64), (300, 256), (10, 12), (40, 1)])
+@pytest.mark.parametrize("n,m", [(1000, 128), (517, 60), (64, 64), (300, 256), (10, 12), (40, 1), (1000, 200),
+                                 (1536, 256)])
 @pytest.mark.parametrize("gen", ["random", "absdiff"])
 @pytest.mark.parametrize("depth", [1, 2, 3, 4, 8])
 def test_engine_single_gpu_vs_numpy(native, n, m, gen, depth):
