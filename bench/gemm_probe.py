@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Single-shape GEMM probe for rocprofv3 counter passes (one kernel shape, fixed repetitions).
 
-    python bench/gemm_probe.py [M N K] [--dtype fp64|fp32] [--variant narrow|big|tall|valu] [--reps R]
+    python bench/gemm_probe.py [M N K] [--dtype fp64|fp32] [--variant narrow|big|bigpf|squarepf|glds|auto] [--reps R]
 
 Prints one JSON line with the achieved rate; meant to run under
 ``rocprofv3 --pmc <counters> -- python3 bench/gemm_probe.py ...``.

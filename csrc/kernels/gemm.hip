@@ -60,17 +60,13 @@ struct Cfg {
   static_assert(NT % BM == 0 && NT % BN == 0, "thread count must tile the slice rows");
   static_assert(SPA >= 1 && SPB >= 1 && MI >= 1 && NJ >= 1, "bad tile config");
 };
-using CfgBig = Cfg<128, 128, 16, 2, 4, 2>;   // 512 threads, 2 WG/CU (73.7 KiB LDS each)
-using CfgNarrow = Cfg<128, 64, 8, 2, 2, 4>;  // 256 threads, 4 WG/CU (28.7 KiB LDS each)
-using CfgTall = Cfg<64, 128, 8, 1, 4, 4>;    // 256 threads, 4 WG/CU
+// The tiles the solver selects (profiles/gemm_variants_k512.md; the round-1 tuning candidates
+// tall / narrowpf / square / wide / big8 / valu were measured slower everywhere and removed):
+using CfgBig = Cfg<128, 128, 16, 2, 4, 2>;   // 512 threads, 2 WG/CU: the residual GEMM
+using CfgNarrow = Cfg<128, 64, 8, 2, 2, 4>;  // 256 threads, 4 WG/CU: K < 384 trailing updates
 using CfgSmall = Cfg<64, 32, 16, 2, 1, 8>;   // 128 threads: latency-bound panel GEMMs (few tiles)
-// tuning candidates (GJ_GEMM_VARIANT)
-using CfgNarrowPf = Cfg<128, 64, 8, 2, 2, 3, 2>;  // narrow, two register stages in flight
-using CfgSquare = Cfg<128, 128, 8, 2, 2, 2>;      // 256 threads, 64x64 per wave (16 MFMA tiles)
-using CfgSquarePf = Cfg<128, 128, 8, 2, 2, 2, 2>;
-using CfgWide = Cfg<256, 128, 8, 4, 2, 1, 2>;     // 512 threads, 64x64 per wave
-using CfgBig8 = Cfg<128, 128, 8, 2, 4, 2, 2>;     // big tile, BK 8, two stages
-using CfgBigPf = Cfg<128, 128, 16, 2, 4, 2, 2>;
+using CfgSquarePf = Cfg<128, 128, 8, 2, 2, 2, 2>;  // fp32 deep trailing updates (110.5 TF/s)
+using CfgBigPf = Cfg<128, 128, 16, 2, 4, 2, 2>;    // fp64 deep updates the LDS-DMA kernel cannot take
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
@@ -603,14 +599,8 @@ static void launch_glds(const GemmArgs& a0, hipStream_t s) {
   a.group = group;
   const dim3 grid((unsigned)nwg), blk(glds::NT);
   switch (stages) {  // LDS per workgroup: 13.3 KiB per stage
-    case 2: hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 4, 8>), grid, blk, 0, s, a); break;
-    case 6: hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 5, 8>), grid, blk, 0, s, a); break;  // 2 stages, 5 WG/CU
-    case 7: hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 3, 16>), grid, blk, 0, s, a); break;  // 16-deep slices
-    case 9: hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 3, 8>), grid, blk, 0, s, a); break;   // 3 WG/CU
-    case 8: hipLaunchKernelGGL((gemm_glds_f64<MODE, 3, 2, 16>), grid, blk, 0, s, a); break;
-    case 4: hipLaunchKernelGGL((gemm_glds_f64<MODE, 4, 3, 8>), grid, blk, 0, s, a); break;
-    case 5: hipLaunchKernelGGL((gemm_glds_f64<MODE, 5, 2, 8>), grid, blk, 0, s, a); break;
-    default: hipLaunchKernelGGL((gemm_glds_f64<MODE, 3, 4, 8>), grid, blk, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 4, 8>), grid, blk, 0, s, a); break;  // 4 WG/CU
+    default: hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 3, 8>), grid, blk, 0, s, a); break;  // 3 WG/CU
   }
 }
 
@@ -643,9 +633,9 @@ static int gemm_variant() {
 }
 int gemm_variant_id(const char* name) {
   const std::string s(name);
-  static const char* names[] = {"big", "narrow", "tall", "valu", "narrowpf", "square", "squarepf", "wide", "big8", "bigpf", "auto", "glds"};
+  static const char* names[] = {"big", "narrow", "", "", "", "", "squarepf", "", "", "bigpf", "auto", "glds"};
   for (int i = 0; i < (int)(sizeof(names) / sizeof(names[0])); ++i)
-    if (s == names[i]) return i;
+    if (*names[i] && s == names[i]) return i;
   return kAutoVariant;
 }
 void set_gemm_variant(int v) { g_variant = v; }
@@ -678,13 +668,7 @@ static void launch(const GemmArgs& a, hipStream_t s) {
   }
   switch (v) {
     case 1: return launch_cfg<T, AL, MODE, CfgNarrow>(a, s);
-    case 2: return launch_cfg<T, AL, MODE, CfgTall>(a, s);
-    case 3: return launch_cfg<T, AL, MODE, CfgNarrow>(a, s);  // valu is fp64/K-major only
-    case 4: return launch_cfg<T, AL, MODE, CfgNarrowPf>(a, s);
-    case 5: return launch_cfg<T, AL, MODE, CfgSquare>(a, s);
     case 6: return launch_cfg<T, AL, MODE, CfgSquarePf>(a, s);
-    case 7: return launch_cfg<T, AL, MODE, CfgWide>(a, s);
-    case 8: return launch_cfg<T, AL, MODE, CfgBig8>(a, s);
     case 9: return launch_cfg<T, AL, MODE, CfgBigPf>(a, s);
     default: return launch_cfg<T, AL, MODE, CfgBig>(a, s);
   }
@@ -705,8 +689,6 @@ void gemm(DType dt, int op, int a_kmajor, int64_t M, int64_t N, int64_t K, const
           int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, hipStream_t s,
           const GemmExtra* ex) {
   if (M <= 0 || N <= 0) return;
-  if (dt == DType::F64 && a_kmajor && gemm_variant() == 3)
-    return gemm_valu(op, M, N, K, A, lda, B, ldb, C, ldc, s, ex);
   GemmArgs a{};
   a.M = M; a.N = N; a.K = K; a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.C = C; a.ldc = ldc;
   fill_extra(a, ex);

@@ -18,10 +18,7 @@ void gemm(DType dt, int op /*0 acc, 1 store*/, int a_kmajor, int64_t M, int64_t 
 // n independent small K-major GEMMs, one launch per 4 (small tiles; Store = C never read)
 void gemm_batch(DType dt, const GemmDesc* d, int n, hipStream_t s);
 int residual_nparts(int64_t N);
-// VALU fp64 variant (gemm_valu.hip), K-major A only
-void gemm_valu(int op, int64_t M, int64_t N, int64_t K, const void* At, int64_t lda, const void* B,
-               int64_t ldb, void* C, int64_t ldc, hipStream_t s, const GemmExtra* ex);
-int gemm_variant_id(const char* name);  // big | narrow | tall | valu
+int gemm_variant_id(const char* name);  // big | narrow | squarepf | bigpf | glds | auto
 void set_gemm_variant(int v);
 void set_block_inverse_variant(int v);  // 0/3/4 = matrix-core panels (pipelined / LDS / readlane row bcast), 1 = sweep, 2 = one-wave panels
 int block_inverse_variant();

@@ -124,7 +124,7 @@ def test_row_abs_max_and_residual():
     assert r < 1e-10 and abs(r - ref) < 1e-11
 
 
-GEMM_VARIANTS = ["big", "narrow", "tall", "valu", "narrowpf", "square", "squarepf", "wide", "big8", "bigpf", "auto", "glds"]
+GEMM_VARIANTS = ["big", "narrow", "squarepf", "bigpf", "auto", "glds"]
 
 
 @pytest.mark.parametrize("variant", GEMM_VARIANTS)
@@ -133,8 +133,6 @@ GEMM_VARIANTS = ["big", "narrow", "tall", "valu", "narrowpf", "square", "squarep
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_gemm_variants_elimination_extras(native, variant, M, N, K, dtype):
     """All kernel variants: C += A B where C enters as 0 in a column range and in two row blocks."""
-    if variant == "valu" and dtype == torch.float32:
-        pytest.skip("the VALU variant is fp64-only")
     native.set_gemm_variant(variant)
     try:
         A = _rand((M, K), torch.float64, 11)
