@@ -18,6 +18,8 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
+#include <string>
 
 #include "kernels.hpp"
 #include "wave_ops.hpp"
@@ -650,9 +652,18 @@ __global__ __launch_bounds__(256) void block_inverse_generic(const T* __restrict
   }
 }
 
-static int g_bi_variant = 0;  // 0 = matrix-core panels (default), 1 = per-step sweep, 2 = one-wave panels
+// 0 = matrix-core panels (default), 1 = per-step sweep, 2 = one-wave panels, 3/4 = matrix-core
+// pivot-wave forms, 5 = co-resident L2-image kernel (fp64 32 < m <= 128; GJ_BI_VARIANT=co)
+static int g_bi_variant = -1;
+static int bi_variant() {
+  if (g_bi_variant < 0) {
+    const char* e = getenv("GJ_BI_VARIANT");
+    g_bi_variant = (e && std::string(e) == "co") ? 5 : 0;
+  }
+  return g_bi_variant;
+}
 void set_block_inverse_variant(int v) { g_bi_variant = v; }
-int block_inverse_variant() { return g_bi_variant; }
+int block_inverse_variant() { return bi_variant(); }
 
 template <typename T>
 static void launch_bi(const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,
@@ -662,6 +673,10 @@ static void launch_bi(const void* Lt, int64_t ldl, void* inv_t, double* scores, 
   const unsigned grid = (unsigned)L.nblk;
   const T* lt = static_cast<const T*>(Lt);
   T* it = static_cast<T*>(inv_t);
+  const int g_bi_variant = bi_variant();
+  if (g_bi_variant == 5 && block_inverse_co(sizeof(T) == 8 ? DType::F64 : DType::F32, Lt, ldl, inv_t, scores,
+                                            valid, used, L, thresh, s, scratch))
+    return;
   if ((g_bi_variant == 0 || g_bi_variant == 3 || g_bi_variant == 4) &&
       block_inverse_mfma(sizeof(T) == 8 ? DType::F64 : DType::F32, Lt, ldl, inv_t, scores, valid, used,
                          L, thresh, s, g_bi_variant == 0 ? 2 : g_bi_variant == 4 ? 1 : 0))
@@ -695,6 +710,7 @@ static void launch_bi(const void* Lt, int64_t ldl, void* inv_t, double* scores, 
 static bool generic_path(DType dt, int64_t m) { return dt == DType::F64 ? m > 128 : m > 256; }
 
 size_t block_inverse_scratch_bytes(DType dt, const Layout& L) {
+  if (bi_variant() == 5 && dt == DType::F64 && L.m > 32 && L.m <= 128) return block_inverse_big_scratch_bytes(dt, L);
   if (!generic_path(dt, L.m)) return 0;
   if (const size_t big = block_inverse_big_scratch_bytes(dt, L)) return big;
   return (size_t)L.nblk * L.m * L.m * dtype_size(dt);

@@ -34,7 +34,6 @@ namespace kern {
 
 namespace {
 
-constexpr int kBigNB = 8;     // block waves
 constexpr int kBigLDU = 17;   // padded row of the U / panel images
 
 // v_mfma_f64_16x16x4f64: A lane l = A[l & 15][l >> 4], B lane l = B[l >> 4][l & 15],
@@ -61,18 +60,22 @@ __device__ __forceinline__ double sum16(double v) {  // sum over the 16 lanes of
 
 }  // namespace
 
-template <int MP>
-__global__ __launch_bounds__(64 * (kBigNB + 1)) void block_inverse_big_kernel(
+// MP = padded block order, NB = block waves (+ 1 pivot wave).  <256, 8>: the m <= 256 kernel;
+// <128, 3> / <64, 3>: the CO-RESIDENT form for m <= 128 — 4 waves (one per SIMD), <= 176 VGPRs and
+// ~72 KiB of LDS, i.e. the footprint ONE retiring trailing-update workgroup frees on a CU (4 x 112
+// VGPRs per SIMD of GEMM + 64 spare; 4 x 26 KiB LDS + 56 spare), so a batch of candidate
+// inverses starts inside a running trailing update instead of waiting for whole CUs.
+template <int MP, int NB>
+__global__ __launch_bounds__(64 * (NB + 1)) void block_inverse_l2_kernel(
     const double* __restrict__ Lt, int64_t ldl, double* __restrict__ inv_t, double* __restrict__ scores,
     int32_t* __restrict__ valid, const int32_t* __restrict__ used, int m, int64_t p, int64_t k,
     double thresh, double* __restrict__ scratch, int32_t* __restrict__ piv_out) {
-  constexpr int NB = kBigNB;
-  constexpr int NT = MP / 16;      // tiles per dimension = panels
-  constexpr int CPW = NT / NB;     // column tiles per block wave
-  constexpr int RPL = MP / 64;     // pivot-wave rows per lane
+  constexpr int NT = MP / 16;               // tiles per dimension = panels
+  constexpr int CPW = (NT + NB - 1) / NB;    // column tiles per block wave (ct = wave + NB j < NT)
+  constexpr int RPL = MP / 64;               // pivot-wave rows per lane
   constexpr int LDU = kBigLDU;
   constexpr int RWC = 16 * CPW + 1;
-  static_assert(CPW * NB == NT && CPW >= 1, "MP must be a multiple of 128");
+  static_assert(MP % 64 == 0 && NB <= NT && 2 * LDU >= NB, "geometry");
 
   const int b = blockIdx.x;
   if (used[(int64_t)b * p + k]) {
@@ -163,6 +166,7 @@ __global__ __launch_bounds__(64 * (kBigNB + 1)) void block_inverse_big_kernel(
   // initial image: W = -(Lt block b)^T, identity in the padding
   for (int j = 0; j < CPW; ++j) {
     const int ct = wave + NB * j;
+    if (ct >= NT) break;
     const int jc = 16 * ct + cl;
     const double* src = Lt + (int64_t)jc * ldl + (int64_t)b * m;
     for (int rt = 0; rt < NT; ++rt) {
@@ -187,8 +191,8 @@ __global__ __launch_bounds__(64 * (kBigNB + 1)) void block_inverse_big_kernel(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     for (int e = lane; e < 16 * 16 * CPW; e += 64) {
       const int kk = e / (16 * CPW), cc = e % (16 * CPW);
-      const int col = 16 * (wave + NB * (cc >> 4)) + (cc & 15);
-      Rw[wave][kk][cc] = S[fidx<NT>(rsel[ub][kk], col)];
+      const int ctc = wave + NB * (cc >> 4);
+      if (ctc < NT) Rw[wave][kk][cc] = S[fidx<NT>(rsel[ub][kk], 16 * ctc + (cc & 15))];
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -200,6 +204,7 @@ __global__ __launch_bounds__(64 * (kBigNB + 1)) void block_inverse_big_kernel(
     for (int jj = 0; jj < CPW; ++jj) {
       const int j = jj == 0 ? first : (jj == first ? 0 : jj);
       const int ct = wave + NB * j;
+      if (ct >= NT) continue;
       double* tile0 = S + ((int64_t)ct * 64 + lane) * 4;
       if (ct == q) {  // the panel's own columns: U + E
         const int rs = rsel[ub][cl];
@@ -252,6 +257,7 @@ __global__ __launch_bounds__(64 * (kBigNB + 1)) void block_inverse_big_kernel(
     double rs[4] = {0.0, 0.0, 0.0, 0.0};
     for (int j = 0; j < CPW; ++j) {
       const int ct = wave + NB * j;
+      if (ct >= NT) break;
       const int u = 16 * ct + cl;
       const acc4 x = *reinterpret_cast<const acc4*>(S + ((int64_t)(rt * NT + ct) * 64 + lane) * 4);
       const int o = u < m ? prow[u] : -1;
@@ -279,15 +285,33 @@ bool block_inverse_big(DType dt, const void* Lt, int64_t ldl, void* inv_t, doubl
   if (dt != DType::F64 || m <= 128 || m > 256) return false;
   const unsigned grid = (unsigned)L.nblk;
   if (grid == 0) return true;
-  hipLaunchKernelGGL((block_inverse_big_kernel<256>), dim3(grid), dim3(64 * (kBigNB + 1)), 0, s,
+  hipLaunchKernelGGL((block_inverse_l2_kernel<256, 8>), dim3(grid), dim3(64 * 9), 0, s,
                      static_cast<const double*>(Lt), ldl, static_cast<double*>(inv_t), scores, valid, used, m,
                      L.p, L.k, thresh, static_cast<double*>(scratch), block_inverse_probe());
   return true;
 }
 
+bool block_inverse_co(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,
+                      const int32_t* used, const Layout& L, double thresh, hipStream_t s, void* scratch) {
+  const int m = (int)L.m;
+  if (dt != DType::F64 || m <= 32 || m > 128) return false;
+  const unsigned grid = (unsigned)L.nblk;
+  if (grid == 0) return true;
+  if (m <= 64)
+    hipLaunchKernelGGL((block_inverse_l2_kernel<64, 3>), dim3(grid), dim3(64 * 4), 0, s,
+                       static_cast<const double*>(Lt), ldl, static_cast<double*>(inv_t), scores, valid, used, m,
+                       L.p, L.k, thresh, static_cast<double*>(scratch), block_inverse_probe());
+  else
+    hipLaunchKernelGGL((block_inverse_l2_kernel<128, 3>), dim3(grid), dim3(64 * 4), 0, s,
+                       static_cast<const double*>(Lt), ldl, static_cast<double*>(inv_t), scores, valid, used, m,
+                       L.p, L.k, thresh, static_cast<double*>(scratch), block_inverse_probe());
+  return true;
+}
+
 size_t block_inverse_big_scratch_bytes(DType dt, const Layout& L) {
-  if (dt != DType::F64 || L.m <= 128 || L.m > 256) return 0;
-  return (size_t)std::max<int64_t>(L.nblk, 1) * 256 * 256 * sizeof(double);
+  if (dt != DType::F64 || L.m <= 32 || L.m > 256) return 0;
+  const int64_t MP = L.m <= 64 ? 64 : L.m <= 128 ? 128 : 256;
+  return (size_t)std::max<int64_t>(L.nblk, 1) * MP * MP * sizeof(double);
 }
 
 }  // namespace kern

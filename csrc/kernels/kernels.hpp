@@ -42,6 +42,9 @@ int32_t* block_inverse_probe();
 bool block_inverse_big(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,
                        const int32_t* used, const Layout& L, double thresh, hipStream_t s, void* scratch);
 size_t block_inverse_big_scratch_bytes(DType dt, const Layout& L);
+// the co-resident form (4 waves, fits the slot one trailing-update workgroup frees): fp64 32 < m <= 128
+bool block_inverse_co(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,
+                      const int32_t* used, const Layout& L, double thresh, hipStream_t s, void* scratch);
 // scratch needed by the fp64 m > 128 paths (big kernel / generic sweep)
 size_t block_inverse_scratch_bytes(DType dt, const Layout& L);
 size_t block_inverse_iscratch_bytes(const Layout& L);

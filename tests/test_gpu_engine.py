@@ -100,7 +100,7 @@ def test_axb_and_profile_on_gpu(native, ranks):
     assert ph["trailing_update"]["ms"] > 0 and ph["pivot_search"]["calls"] == (n + m - 1) // m
 
 
-@pytest.mark.parametrize("variant", ["panel", "sweep", "panel1", "panel_lds", "panel_rl"])
+@pytest.mark.parametrize("variant", ["panel", "sweep", "panel1", "panel_lds", "panel_rl", "co"])
 def test_block_inverse_variants_in_engine(native, variant):
     n, m = 640, 128
     A = generate_matrix(n, "random", 21)[::-1].copy()  # forces off-diagonal pivots
