@@ -46,8 +46,13 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   GJ_REQUIRE(n > 0 && m > 0, "n and m must be positive");
   L_ = Layout::make(n, m, comm.size(), comm.rank());
   GJ_REQUIRE(L_.Nr < (int64_t(1) << 31), "too many block rows");
-  // auto depth: profiles/small_n_sweep.md (N=8192: depth 2 34.6 vs 35.9 ms; N=16384: 4 wins)
-  const int want = opt_.depth > 0 ? opt_.depth : (L_.npad <= 8192 ? 2 : 4);
+  // auto depth: profiles/small_n_sweep.md (N=8192: depth 2 34.6 vs 35.9 ms; N=16384: 4 wins), and
+  // 8 on ranks of <= 4096 rows of a large matrix (p = 8 at N = 32768: K = 1024 halves the panel
+  // boundaries the pivot chain must hide behind a short trailing update; emulated under the
+  // communication-cost model 0.167 vs 0.177 s, while depth 6 / 8 lose at p = 1 / 2 / 4 and at
+  // N = 16384: profiles/depth_pgt1.md)
+  const bool small_rank = L_.p > 1 && L_.max_nblk * L_.m <= 4096;
+  const int want = opt_.depth > 0 ? opt_.depth : (L_.npad <= 8192 ? 2 : (small_rank && L_.npad > 16384) ? 8 : 4);
   d_ = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)want, (int64_t)kMaxDepth, L_.Nr}));
 
   // Column chunk plan: fixed partition of the Nr block columns into runs of a multiple of d blocks.
@@ -116,8 +121,7 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // with <= 4096 rows (p = 8 at N = 32768), where the pivot chain and the RCCL workgroups of its
   // collectives need the free CUs: under the communication-cost model p = 8 is 6.6 % faster with
   // the reservation at 100 GB/s, p = 2 / 4 are 9 / 6 % slower (profiles/cu_reserve_pgt1.md).
-  if (rc < 0)
-    rc = (dev_.on_gpu() && (L_.npad <= 16384 || (L_.p > 1 && L_.max_nblk * L_.m <= 4096))) ? 32 : 0;
+  if (rc < 0) rc = (dev_.on_gpu() && (L_.npad <= 16384 || small_rank)) ? 32 : 0;
   dev_.reserve_cus(rc, opt_.reserve_mode);
 }
 
