@@ -81,6 +81,8 @@ class AsyncHostDevice : public Device {
   void permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx, int64_t nblk,
                       int64_t m, int64_t Nr, const int32_t* dst_blk, const int32_t* colsrc,
                       int s) override;
+  void row_abs_max_minus_i(DType dt, const void* X, int64_t ldx, const Layout& L, double* out,
+                           int s) override;
   void row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out,
                    int s) override;
   void residual(DType dt, const void* A, const void* Full, const Layout& L, double* out,

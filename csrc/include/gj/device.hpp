@@ -182,6 +182,9 @@ class Device {
   // out[0] = max over local real rows of sum_{j<n} |X[r][j]|  (reference norm(), main.cpp:643-667).
   virtual void row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out,
                            int s) = 0;
+  // out[0] = max over local real rows r of sum_{j<n} |X[r][j] - delta(global(r), j)|
+  virtual void row_abs_max_minus_i(DType dt, const void* X, int64_t ldx, const Layout& L, double* out,
+                                   int s) = 0;
   // out[0] = max over local real rows r of sum_{j<n} |(A_loc * Full)[r][j] - delta(global(r), j)|
   // (matrix_mult_matrix + minus_i + norm, main.cpp:534-667, fused).  A_loc row-major ld npad,
   // Full = the whole inverse in natural row order (npad x npad).

@@ -160,6 +160,7 @@ class Engine {
   void big_update(int64_t u);
   void finalize(const std::vector<int32_t>& seq);
   double residual_common(const void* A, bool wide);
+  double residual_streamed(const void* A, bool wide);
   bool residual_wide();
   size_t residual_fp64_bytes() const;
   void upload_rows_into(void* P, DType dt, const double* host, int64_t ld);

@@ -73,7 +73,9 @@ void h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, hipStrea
 void permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx, int64_t nblk,
                     int64_t m, int64_t Nr, const int32_t* dst_blk, const int32_t* colsrc,
                     hipStream_t s);
-void row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out, hipStream_t s);
+// minus_identity: sum_j |X[r][j] - delta(global(r), j)| (the streamed residual's row sums)
+void row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out, hipStream_t s,
+                 bool minus_identity = false);
 // reduce residual partials: out = max over real local rows of sum_parts partial[r][*]
 void residual_reduce(const double* partial, int nparts, const Layout& L, double* out, hipStream_t s);
 

@@ -378,12 +378,13 @@ void permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx
 // ---------------------------------------------------------------- norms
 template <typename T>
 __global__ __launch_bounds__(256) void row_abs_kernel(const T* X, int64_t ldx, int64_t n, int64_t m,
-                                                      int64_t p, int64_t k, double* out) {
+                                                      int64_t p, int64_t k, double* out, int minus_i) {
   const int64_t r = blockIdx.x;
   const int64_t gr = ((r / m) * p + k) * m + r % m;
   if (gr >= n) return;
   double s = 0.0;
-  for (int64_t j = threadIdx.x; j < n; j += 256) s += fabs((double)X[r * ldx + j]);
+  for (int64_t j = threadIdx.x; j < n; j += 256)
+    s += fabs((double)X[r * ldx + j] - ((minus_i && j == gr) ? 1.0 : 0.0));
   __shared__ double sh[4];
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
@@ -392,15 +393,17 @@ __global__ __launch_bounds__(256) void row_abs_kernel(const T* X, int64_t ldx, i
   if (threadIdx.x == 0) atomic_max_nonneg(out, sh[0] + sh[1] + sh[2] + sh[3]);
 }
 
-void row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out, hipStream_t s) {
+void row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out, hipStream_t s,
+                 bool minus_identity) {
   (void)hipMemsetAsync(out, 0, sizeof(double), s);
   if (L.rows <= 0) return;
+  const int mi = minus_identity ? 1 : 0;
   if (dt == DType::F64)
     hipLaunchKernelGGL(row_abs_kernel<double>, dim3((unsigned)L.rows), dim3(256), 0, s,
-                       static_cast<const double*>(X), ldx, L.n, L.m, L.p, L.k, out);
+                       static_cast<const double*>(X), ldx, L.n, L.m, L.p, L.k, out, mi);
   else
     hipLaunchKernelGGL(row_abs_kernel<float>, dim3((unsigned)L.rows), dim3(256), 0, s,
-                       static_cast<const float*>(X), ldx, L.n, L.m, L.p, L.k, out);
+                       static_cast<const float*>(X), ldx, L.n, L.m, L.p, L.k, out, mi);
 }
 
 __global__ __launch_bounds__(256) void residual_reduce_kernel(const double* partial, int nparts,

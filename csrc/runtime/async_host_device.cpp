@@ -269,6 +269,10 @@ void AsyncHostDevice::permute_blocks(DType dt, void* dst, int64_t ldd, const voi
                                      const int32_t* colsrc, int s) {
   enqueue(s, [=] { inner_.permute_blocks(dt, dst, ldd, X, ldx, nblk, m, Nr, dst_blk, colsrc, s); });
 }
+void AsyncHostDevice::row_abs_max_minus_i(DType dt, const void* X, int64_t ldx, const Layout& L, double* out,
+                                          int s) {
+  enqueue(s, [=] { inner_.row_abs_max_minus_i(dt, X, ldx, L, out, s); });
+}
 void AsyncHostDevice::row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out,
                                   int s) {
   enqueue(s, [=] { inner_.row_abs_max(dt, X, ldx, L, out, s); });

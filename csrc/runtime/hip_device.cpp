@@ -287,6 +287,11 @@ void HipDevice::permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, 
   kern::permute_blocks(dt, dst, ldd, X, ldx, nblk, m, Nr, dst_blk, colsrc, hs(streams_[s]));
   check_launch();
 }
+void HipDevice::row_abs_max_minus_i(DType dt, const void* X, int64_t ldx, const Layout& L, double* out,
+                                    int s) {
+  kern::row_abs_max(dt, X, ldx, L, out, hs(streams_[s]), true);
+  check_launch();
+}
 void HipDevice::row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out,
                             int s) {
   kern::row_abs_max(dt, X, ldx, L, out, hs(streams_[s]));

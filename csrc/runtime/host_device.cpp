@@ -338,6 +338,22 @@ void HostDevice::permute_blocks(DType dt, void* dst, int64_t ldd, const void* X,
   });
 }
 
+void HostDevice::row_abs_max_minus_i(DType dt, const void* X, int64_t ldx, const Layout& L, double* out,
+                                     int) {
+  double mx = 0.0;
+  for (int64_t r = 0; r < L.rows; ++r) {
+    const int64_t gr = L.global_row(r);
+    if (gr >= L.n) continue;
+    double s = 0.0;
+    for (int64_t j = 0; j < L.n; ++j) {
+      const double v = dt == DType::F64 ? tp<double>(X)[r * ldx + j] : (double)tp<float>(X)[r * ldx + j];
+      s += std::fabs(v - (j == gr ? 1.0 : 0.0));
+    }
+    mx = std::max(mx, s);
+  }
+  out[0] = mx;
+}
+
 void HostDevice::row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out,
                              int) {
   double mx = 0.0;

@@ -134,13 +134,21 @@ int64_t Engine::real_local_rows() const {
 }
 
 namespace {
-// GJ_TEST_ALLOC_FAIL=<rank>:<matrix|block> makes that rank's allocation fail (failure-agreement tests).
+// GJ_TEST_ALLOC_FAIL=<rank>:<stage>[,<rank>:<stage>...] makes that rank's allocation of that stage
+// (matrix | block | residual | residual_stream | residual64) fail (failure-agreement tests).
 bool injected_alloc_fail(int rank, const char* stage) {
   const char* e = std::getenv("GJ_TEST_ALLOC_FAIL");
   if (!e || !*e) return false;
-  const std::string v = e;
-  const size_t c = v.find(':');
-  return c != std::string::npos && std::atoi(v.substr(0, c).c_str()) == rank && v.substr(c + 1) == stage;
+  const std::string all = e;
+  size_t b = 0;
+  while (b <= all.size()) {
+    const size_t end = std::min(all.find(',', b), all.size());
+    const std::string v = all.substr(b, end - b);
+    const size_t c = v.find(':');
+    if (c != std::string::npos && std::atoi(v.substr(0, c).c_str()) == rank && v.substr(c + 1) == stage) return true;
+    b = end + 1;
+  }
+  return false;
 }
 }  // namespace
 
@@ -907,9 +915,7 @@ double Engine::residual_common(const void* A, bool wide) {
     const size_t need = (size_t)npad * npad * es + per * p + (L_.nblk < L_.max_nblk ? per : 0);
     const bool fits = !injected_alloc_fail(L_.k, "residual") &&
                       (!dev_.on_gpu() || need + (64u << 20) <= dev_.free_memory());
-    if (comm_.host_max(dev_, fits ? 0.0 : 1.0) > 0)
-      throw Error(Status::NoMemory, "not enough device memory for the residual's gathered inverse (" +
-                                        std::to_string(need) + " bytes per rank)");
+    if (comm_.host_max(dev_, fits ? 0.0 : 1.0) > 0) return residual_streamed(A, wide);
     full = dev_.alloc((size_t)npad * npad * es);
     gath = dev_.alloc(per * p);
     void* send = out_;
@@ -948,6 +954,60 @@ double Engine::residual_common(const void* A, bool wide) {
   dev_.sync_stream(S_MAIN);
   if (fullr != full) dev_.release(fullr);
   if (p > 1) dev_.release(full);
+  last_residual_fp64_ = (rdt == DType::F64);
+  return comm_.host_max(dev_, local);
+}
+
+// p > 1 when the whole inverse does not fit on some rank: the reference's ring (matrix_mult_matrix,
+// main.cpp:534-642, MPI_Sendrecv_replace of the B strips) as p broadcasts of one rank's strip at a
+// time.  R = A_loc * inv accumulates strip by strip (strip q = block rows j p + q of the inverse
+// meet columns (j p + q) m .. + m of A_loc), then sum_j |R - I| per row.  Needs R, one strip and
+// (fp32 solves checked in fp64) its widened copy instead of two whole inverses.
+double Engine::residual_streamed(const void* A, bool wide) {
+  const int64_t m = L_.m, p = L_.p, npad = L_.npad, rows = std::max<int64_t>(L_.rows, 1);
+  const size_t es = esz();
+  const DType rdt = wide ? DType::F64 : opt_.dtype;
+  const size_t res = dtype_size(rdt);
+  const size_t per = (size_t)L_.max_nblk * m * npad;  // elements of the largest strip
+  const size_t need = (size_t)rows * npad * res + per * es + (wide ? per * 8 : 0);
+  const bool fits = !injected_alloc_fail(L_.k, "residual_stream") &&
+                    (!dev_.on_gpu() || need + (64u << 20) <= dev_.free_memory());
+  if (comm_.host_max(dev_, fits ? 0.0 : 1.0) > 0)
+    throw Error(Status::NoMemory, "not enough device memory for the residual (" + std::to_string(need) +
+                                      " bytes per rank even streamed)");
+  const int s = S_COMM;  // the broadcasts' stream: every GEMM after its strip without a cross-stream hop
+  void* R = dev_.alloc((size_t)rows * npad * res);
+  void* S = dev_.alloc(per * es);
+  void* Sw = wide ? dev_.alloc(per * 8) : nullptr;
+  dev_.record(ev_main_, S_MAIN);  // A (MAIN) is complete before the first product
+  dev_.wait(s, ev_main_);
+  dev_.memset0(R, (size_t)rows * npad * res, s);
+  for (int64_t q = 0; q < p; ++q) {
+    const int64_t nbq = rows_owned(L_.Nr, p, q);
+    if (nbq == 0) continue;
+    void* buf = (q == L_.k) ? out_ : S;
+    comm_.bcast(dev_, buf, (size_t)nbq * m * npad * es, (int)q, s);
+    const void* src = buf;
+    if (wide) {
+      dev_.widen(opt_.dtype, static_cast<double*>(Sw), npad, buf, npad, nbq * m, npad, s);
+      src = Sw;
+    }
+    if (L_.nblk > 0)
+      for (int64_t j = 0; j < nbq; ++j)
+        dev_.gemm(rdt, GemmOp::Acc, ALayout::RowMajor, L_.rows, npad, m,
+                  static_cast<const char*>(A) + (size_t)(j * p + q) * m * res, npad,
+                  static_cast<const char*>(src) + (size_t)j * m * npad * res, npad, R, npad, s);
+  }
+  double local = 0.0;
+  if (L_.nblk > 0) {
+    dev_.row_abs_max_minus_i(rdt, R, npad, L_, dscratch_, s);
+    dev_.copy(dhost_, dscratch_, sizeof(double), s);
+  }
+  comm_.drain(dev_, s);
+  if (L_.nblk > 0) local = dhost_[0];
+  dev_.release(R);
+  dev_.release(S);
+  if (Sw) dev_.release(Sw);
   last_residual_fp64_ = (rdt == DType::F64);
   return comm_.host_max(dev_, local);
 }
