@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--ranks", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--size", type=int, default=32768)
     ap.add_argument("--block", type=int, default=128)
-    ap.add_argument("--depth", type=int, nargs="+", default=[4])
+    ap.add_argument("--depth", type=int, nargs="+", default=[0], help="0 = the engine's auto choice")
     ap.add_argument("--dtype", default="fp64")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--chunk-cols", type=int, default=0)
@@ -56,23 +56,23 @@ def main():
             times.append(time.perf_counter() - t0)
             if p > 1:
                 modelled = (C.shadow_modelled_us(comm) - m0) * 1e-6
-        rows = eng.layout["rows"]
+        rows, depth = eng.layout["rows"], eng.layout["depth"]
         del eng
-        return min(times[1:]), st, rows, modelled
+        return min(times[1:]), st, (rows, depth), modelled
 
     for p in args.ranks:
         for d in args.depth:
-            t_free, st, rows, _ = run(p, d, 0.0)
+            t_free, st, (rows, dd), _ = run(p, d, 0.0)
             gemm_flops = 2.0 * rows * args.size * args.size  # this rank's share of 2N^3
-            print(json.dumps({"p": p, "depth": d, "n": args.size, "m": args.block, "status": st["status"],
+            print(json.dumps({"p": p, "depth": dd, "n": args.size, "m": args.block, "status": st["status"],
                               "seconds": round(t_free, 4),
                               "job_gflops_if_comm_free": round(2 * args.size ** 3 / t_free / 1e9, 1),
                               "rank_tflops": round(gemm_flops / t_free / 1e12, 2),
                               "host_wait_ms": round(st["host_wait_ms"], 1)}), flush=True)
             for bw in (args.bw if p > 1 else []):
-                t, st, rows, modelled = run(p, d, bw)
+                t, st, (rows, dd), modelled = run(p, d, bw)
                 hidden = 1.0 - (t - t_free) / modelled if modelled > 0 else None
-                print(json.dumps({"p": p, "depth": d, "n": args.size, "model_bw_gbs": bw, "model_lat_us": args.lat,
+                print(json.dumps({"p": p, "depth": dd, "n": args.size, "model_bw_gbs": bw, "model_lat_us": args.lat,
                                   "model_channels": args.channels, "status": st["status"],
                                   "seconds": round(t, 4),
                                   "job_gflops_cost_model": round(2 * args.size ** 3 / t / 1e9, 1),
