@@ -163,3 +163,24 @@ def test_bcast_flag(gj_bin, mode):
 def test_bcast_flag_rejects_unknown(gj_bin):
     rc, out, _ = run(gj_bin, "--bcast", "tree", 10, 3)
     assert rc == 1
+
+
+def test_not_enough_memory_messages(gj_bin, monkeypatch):
+    # the matrix itself (main.cpp:366-381): before any output; the work space (main.cpp:428-436):
+    # after the A corner, like the reference's Jordan() failure
+    monkeypatch.setenv("GJ_TEST_ALLOC_FAIL", "1:matrix")
+    rc, out, _ = run(gj_bin, "-p", 3, 40, 8)
+    assert rc == 2 and out == "Not enough memory!\n"
+    monkeypatch.setenv("GJ_TEST_ALLOC_FAIL", "2:block")
+    rc, out, _ = run(gj_bin, "-p", 3, 40, 8)
+    assert rc == 2 and out.startswith("A\n") and out.endswith("not enough memory for block\n")
+
+
+def test_fp32_refinement_json(gj_bin):
+    import json
+    rc, out, err = run(gj_bin, "--dtype", "fp32", "--gen", "randshift", "--rhs", "ones", "--refine", 5, "--json",
+                       300, 16)
+    assert rc == 0 and "Ax-b residual:" in out
+    d = json.loads(err.strip().splitlines()[-1])
+    assert d["residual_fp64"] is True and d["refine_converged"] is True
+    assert d["axb_history"][-1] < 1e-12 and d["refine_steps"] >= 1
