@@ -430,7 +430,7 @@ __device__ __forceinline__ void wait_pieces(int n) {
   }
 }
 
-template <int MODE, int NS, int OCC, int BK, bool COVL = true>
+template <int MODE, int NS, int OCC, int BK>
 __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
   using namespace glds;
   static_assert(NS >= 2 && NS <= 5, "stages");
@@ -496,19 +496,13 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
         }
       }
     }
-  // C must have landed before the hand-written waits below count the LDS-DMA pieces.  COVL: the
-  // prologue slices are issued first and C is waited for behind them (the compiler's wait for the
-  // acc registers leaves the newer DMA pieces in flight), so the C-tile and first-slice latencies
-  // overlap instead of adding up once per tile.
-  auto c_landed = [&]() {
+  // C must have landed before the first LDS-DMA is counted by the hand-written waits below
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) asm volatile("" ::"v"(acc[i][j][q]));
-  };
-  if constexpr (!COVL) c_landed();
+      for (int q = 0; q < 4; ++q) asm volatile("" ::"v"(acc[i][j][q]));
 
   // DMA piece geometry (per wave, per slice): A rows wid and wid + 4 (lane l -> columns 2l, 2l+1);
   // B rows 2 wid + (l >> 5), columns 2 (l & 31) of the swizzled image.
@@ -559,7 +553,6 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
   const int nk = (int)((g.K + BK - 1) / BK);
   const int pro = nk < NS - 1 ? nk : NS - 1;  // slices issued ahead
   for (int kt = 0; kt < pro; ++kt) issue(kt);
-  if constexpr (COVL) c_landed();
   wait_pieces<PIECES>(pro - 1);  // slice 0 landed
   __builtin_amdgcn_s_barrier();
   for (int kt = 0; kt < nk; ++kt) {
@@ -605,13 +598,9 @@ static void launch_glds(const GemmArgs& a0, hipStream_t s) {
   static const int group = getenv("GJ_GEMM_GROUP") ? atoi(getenv("GJ_GEMM_GROUP")) : 4;
   a.group = group;
   const dim3 grid((unsigned)nwg), blk(glds::NT);
-  static const bool covl = !(getenv("GJ_GLDS_COVL") && atoi(getenv("GJ_GLDS_COVL")) == 0);
   switch (stages) {  // LDS per workgroup: 13.3 KiB per stage
     case 2: hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 4, 8>), grid, blk, 0, s, a); break;  // 4 WG/CU
-    default:
-      if (covl) hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 3, 8, true>), grid, blk, 0, s, a);   // 3 WG/CU
-      else hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 3, 8, false>), grid, blk, 0, s, a);
-      break;
+    default: hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 3, 8>), grid, blk, 0, s, a); break;  // 3 WG/CU
   }
 }
 
