@@ -11,17 +11,21 @@
 //                                          minus_i + norm, main.cpp:534-667, fused: no D matrix)
 //
 // Kernels (all wave64, v_mfma_f64_16x16x4_f64 with C/D map col = lane&15, row = (lane>>4) + 4*reg
-// for fp64; v_mfma_f32_16x16x4_f32, row = 4*(lane>>4) + reg, for fp32; the accumulator is loaded
-// straight from C in the C/D layout, so the read-modify-write needs no separate epilogue pass):
+// for fp64; v_mfma_f32_16x16x4_f32, row = 4*(lane>>4) + reg, or v_mfma_f32_32x32x2_f32 for fp32;
+// the accumulator is loaded straight from C in the C/D layout, so the read-modify-write needs no
+// separate epilogue pass):
 //   * gemm_glds_f64 — the fp64 trailing update (K = depth*m >= 384, enough tiles to fill the chip):
 //     128 x 64 tile per 256-thread workgroup, 2 x 2 waves of 64 x 32, operands staged global -> LDS
 //     by LDS-DMA (buffer_load_dwordx4 ... lds) into a 2-stage ring, counted vmcnt + raw s_barrier,
 //     4 workgroups per CU (82 % MFMA busy at 2.3 GHz: profiles/gemm_variants_k512.md).
-//   * gemm_kernel<T, A-layout, MODE, Cfg> — register-staged tiles for everything else (fp32 deep
-//     updates use the 128 x 128 "squarepf" tile, 110 TF/s; latency-bound panel GEMMs the small
-//     64 x 32 tile; the residual the 128 x 128 tile).  K is staged through LDS in BK-deep slices,
-//     double-buffered, with a 16-element row pad so the fragment reads (lanes 0-15 / 16-31 on
-//     consecutive k rows) are bank-conflict free; Cfg::PF = 2 keeps two slices in registers.
+//   * gemm_glds_f32 — the fp32 trailing update: the same LDS-DMA ring, 128 x 128 tile of 2 x 2
+//     waves of 64 x 64, v_mfma_f32_32x32x2_f32, 126-132 TF/s (squarepf register staging 118-122).
+//   * gemm_kernel<T, A-layout, MODE, Cfg> — register-staged tiles for everything else
+//     (latency-bound panel GEMMs the small 64 x 32 tile; the residual the 128 x 128 tile; fp32
+//     deep updates the glds32 kernel cannot take the 128 x 128 "squarepf" tile).  K is staged
+//     through LDS in BK-deep slices, double-buffered, with a 16-element row pad so the fragment
+//     reads (lanes 0-15 / 16-31 on consecutive k rows) are bank-conflict free; Cfg::PF = 2 keeps
+//     two slices in registers.
 // All global traffic uses buffer instructions on a per-tile (or per-slice) resource with one 32-bit
 // per-lane offset plus SGPR offsets (no 64-bit address registers, no spills), and masking is done
 // with out-of-range offsets instead of branches (see kOOB).  Tiles are mapped XCD-aware (xcd_remap).
@@ -561,6 +565,9 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
     // slice kt+1 must have landed (this wave's pieces); the later issued ones may stay in flight
     const int last = (kt + NS - 1 < nk ? kt + NS - 1 : nk - 1);
     wait_pieces<PIECES>(last - (kt + 1) > 0 ? last - (kt + 1) : 0);
+    // every wave's fragment reads of this stage complete before the barrier that lets a wave
+    // refill it (hipcc sinks the last reads' wait below a raw s_barrier; measured free)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
 
@@ -608,6 +615,214 @@ static bool glds_ok(const GemmArgs& a) {
   const auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   return a.M % 2 == 0 && a.N % 2 == 0 && a.lda % 2 == 0 && a.ldb % 2 == 0 && al16(a.A) && al16(a.B) &&
          a.lda * a.K * 8 < kRecords && a.ldb * a.K * 8 < kRecords && a.ldc * 128 * 8 < kRecords;
+}
+
+// ---- fp32 trailing-update GEMM: the same LDS-DMA ring, built around v_mfma_f32_32x32x2_f32.
+//
+// The 32 x 32 x 2 instruction does the work of two 16 x 16 x 4 ones for the same two operand
+// floats per lane, so a 64 x 64 wave tile (2 x 2 instructions) reads 4 LDS dwords per 256 MFMA
+// cycles.  Its fragment reads are 32 consecutive floats of one k row per half-wave (the two lane
+// groups of ds_read_b32), conflict-free without a pad or swizzle, so the LDS image of a slice is
+// the plain [k][128] copy of A (K-major) and of B, and one 16-byte-per-lane DMA piece moves two
+// whole k rows.  128 x 128 tile per 256-thread workgroup (2 x 2 waves).  Accumulator map of the
+// 32 x 32 instruction: column lane & 31, register r -> row 8 (r >> 2) + 4 (lane >> 5) + (r & 3).
+// Requirements (checked by glds32_ok): K-major A; M, N, lda, ldb multiples of 4; A/B 16-B aligned.
+namespace glds32 {
+constexpr int BM = 128, BN = 128, NT = 256;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <int P>
+__device__ __forceinline__ void wait_slices(int n) {  // the pieces of the n newest slices may fly
+  if (n <= 0) wait_vm<0>();
+  else if (n == 1) wait_vm<P>();
+  else if (n == 2) wait_vm<2 * P>();
+  else wait_vm<3 * P>();
+}
+
+template <int MODE, int NS, int OCC, int BK>
+__global__ __launch_bounds__(glds32::NT, OCC) void gemm_glds_f32(GemmArgs g) {
+  using namespace glds32;
+  static_assert(NS >= 2 && NS <= 4, "stages");
+  static_assert(BK == 8 || BK == 16 || BK == 32, "slice depth");
+  constexpr int SA = BK * BM, SB = BK * BN, STAGE = SA + SB;
+  constexpr int PIECES = BK / 8 + BK / 8;  // per wave per slice: A rows, B rows (2 per piece)
+  typedef float acc_t __attribute__((ext_vector_type(16)));
+  constexpr int ES = 4, TM = 64, TN = 64, MI = 2, NJ = 2, WN = 2;
+  __shared__ float lds[NS * STAGE];
+
+  const int nwg = g.tiles_m * g.tiles_n;
+  const int tile = xcd_remap((int)blockIdx.x, nwg);
+  const int G = g.group > 0 ? g.group : 1;
+  const int grp = tile / (G * g.tiles_n), gr0 = grp * G;
+  const int gsz = (g.tiles_m - gr0) < G ? (g.tiles_m - gr0) : G;
+  const int rem = tile - grp * G * g.tiles_n;
+  const int tm = gr0 + rem % gsz, tn = rem / gsz;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const float* A = static_cast<const float*>(g.A);
+  const float* B = static_cast<const float*>(g.B);
+  float* C = static_cast<float*>(g.C);
+  const int ldc = (int)g.ldc, ldb = (int)g.ldb, lda = (int)g.lda;
+
+  const int rlane = wm * TM + 4 * (lane >> 5);
+  const int clane = wn * TN + (lane & 31);
+  const int Mt = (int)((g.M - m0) < BM ? (g.M - m0) : BM);
+  const int Nt = (int)((g.N - n0) < BN ? (g.N - n0) : BN);
+  const int64_t zlo = g.zc0 - n0, zhi = g.zc1 - n0;
+  const int z0 = (int)(zlo < 0 ? 0 : (zlo > BN ? BN : zlo)), z1 = (int)(zhi < 0 ? 0 : (zhi > BN ? BN : zhi));
+  int zr0[GemmExtra::kMaxZeroRows], zr1[GemmExtra::kMaxZeroRows];
+#pragma unroll
+  for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) {
+    const int64_t lo = g.zr[z] - m0, hi = g.zr[z] + g.zh - m0;
+    zr0[z] = (int)(lo < 0 ? 0 : (lo > BM ? BM : lo));
+    zr1[z] = (int)(hi < 0 ? 0 : (hi > BM ? BM : hi));
+  }
+  __amdgpu_buffer_rsrc_t rc = rsrc(C + m0 * g.ldc + n0);
+  const int cvoff = (rlane * ldc + clane) * ES;
+
+  acc_t acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int dr = i * 32 + 8 * (q >> 2) + (q & 3);
+      const int r = rlane + dr;
+      bool zrow = false;
+#pragma unroll
+      for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) zrow |= (r >= zr0[z] && r < zr1[z]);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int c = clane + j * 32;
+        if (MODE == MODE_ACC) {
+          const bool ok = r < Mt && c < Nt && !zrow && !(c >= z0 && c < z1);
+          acc[i][j][q] = bload<float>(rc, ok ? cvoff + j * 32 * ES : kOOB, dr * ldc * ES);
+        } else {
+          acc[i][j][q] = 0.0f;
+        }
+      }
+    }
+  // C must have landed before the first LDS-DMA is counted by the hand-written waits below
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) asm volatile("" ::"v"(acc[i][j][q]));
+
+  // DMA piece (per wave): k rows 2 (wid + 4h) + (lane >> 5), floats 4 (lane & 31) .. + 3
+  const int dcol = 4 * (lane & 31), drow = lane >> 5;
+  const bool a_ok = (m0 + dcol) < g.M, b_ok = (n0 + dcol) < g.N;
+  __amdgpu_buffer_rsrc_t ra = rsrc(A + m0);
+  __amdgpu_buffer_rsrc_t rb = rsrc(B + n0);
+  const int Kd = (int)g.K;
+  auto issue = [&](int kt) {
+    float* st = lds + (kt % NS) * STAGE;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int h = 0; h < BK / 8; ++h) {
+      const int kp = 2 * (wid + 4 * h), kr = kp + drow;
+      const bool ok = a_ok && (k0 + kr) < Kd;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(st + kp * BM), 16,
+                                               ok ? ((k0 + kr) * lda + dcol) * ES : kOOB, 0, 0, 0);
+    }
+#pragma unroll
+    for (int h = 0; h < BK / 8; ++h) {
+      const int kp = 2 * (wid + 4 * h), kr = kp + drow;
+      const bool ok = b_ok && (k0 + kr) < Kd;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (__attribute__((address_space(3))) void*)(st + SA + kp * BN),
+                                               16, ok ? ((k0 + kr) * ldb + dcol) * ES : kOOB, 0, 0, 0);
+    }
+  };
+  // fragments of k step kk + 2 are read while the MFMAs of step kk run (two register sets)
+  auto compute = [&](int kt) {
+    const float* sa = lds + (kt % NS) * STAGE + wm * TM + (lane & 31) + (lane >> 5) * BM;
+    const float* sb = lds + (kt % NS) * STAGE + SA + wn * TN + (lane & 31) + (lane >> 5) * BN;
+    float a[2][MI], b[2][NJ];
+    auto frag = [&](int kk, int s) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a[s][i] = sa[kk * BM + i * 32];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) b[s][j] = sb[kk * BN + j * 32];
+    };
+    frag(0, 0);
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 2) {
+      const int s = (kk >> 1) & 1;
+      if (kk + 2 < BK) frag(kk + 2, s ^ 1);
+      __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the MFMAs
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s][i], b[s][j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  const int nk = (int)((g.K + BK - 1) / BK);
+  const int pro = nk < NS - 1 ? nk : NS - 1;
+  for (int kt = 0; kt < pro; ++kt) issue(kt);
+  wait_slices<PIECES>(pro - 1);
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + NS - 1 < nk) issue(kt + NS - 1);
+    compute(kt);
+    const int last = (kt + NS - 1 < nk ? kt + NS - 1 : nk - 1);
+    wait_slices<PIECES>(last - (kt + 1) > 0 ? last - (kt + 1) : 0);
+    // every wave's fragment reads of this stage are complete before anyone refills it
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int dr = i * 32 + 8 * (q >> 2) + (q & 3);
+      const int r = rlane + dr;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int c = clane + j * 32;
+        bstore(acc[i][j][q], rc, (r < Mt && c < Nt) ? cvoff + j * 32 * ES : kOOB, dr * ldc * ES);
+      }
+    }
+}
+
+template <int MODE>
+static void launch_glds32(const GemmArgs& a0, hipStream_t s) {
+  GemmArgs a = a0;
+  a.tiles_m = (int)((a.M + glds32::BM - 1) / glds32::BM);
+  a.tiles_n = (int)((a.N + glds32::BN - 1) / glds32::BN);
+  const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;
+  if (nwg <= 0) return;
+  static const int cfg = getenv("GJ_GLDS32") ? atoi(getenv("GJ_GLDS32")) : 0;
+  static const int group = getenv("GJ_GEMM_GROUP") ? atoi(getenv("GJ_GEMM_GROUP")) : 4;
+  a.group = group;
+  const dim3 grid((unsigned)nwg), blk(glds32::NT);
+  // <stages, launch-bounds workgroups per CU, slice depth>; 8 KiB of LDS per 8 k rows.  Measured
+  // (scripts/f32_ab.sh, TF/s at 32768x16384x512 / 16384x65536x512 / 4096x65536x1024): <2,3,16>
+  // 125.9 / 128.5 / 132.4 (4 WG/CU at 114 VGPRs), <2,2,16> 122.1 / 128.1 / 133.1, <3,2,16> 122.5 /
+  // 125.0 / 129.1, <2,3,8> 125.3 / 127.7 / 131.4, <2,2,32> 116.2 / 118.4 / 124.1; squarepf 117.8 /
+  // 119.8 / 122.3.
+  switch (cfg) {
+    case 1: hipLaunchKernelGGL((gemm_glds_f32<MODE, 2, 2, 16>), grid, blk, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((gemm_glds_f32<MODE, 3, 2, 16>), grid, blk, 0, s, a); break;
+    case 3: hipLaunchKernelGGL((gemm_glds_f32<MODE, 2, 3, 8>), grid, blk, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((gemm_glds_f32<MODE, 2, 2, 32>), grid, blk, 0, s, a); break;
+    default: hipLaunchKernelGGL((gemm_glds_f32<MODE, 2, 3, 16>), grid, blk, 0, s, a); break;
+  }
+}
+
+static bool glds32_ok(const GemmArgs& a) {
+  const auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  return a.M % 4 == 0 && a.N % 4 == 0 && a.lda % 4 == 0 && a.ldb % 4 == 0 && al16(a.A) && al16(a.B) &&
+         a.lda * a.K * 4 < kRecords && a.ldb * a.K * 4 < kRecords && a.ldc * 128 * 4 < kRecords;
 }
 
 template <typename T, int AL, int MODE, typename CF>
@@ -658,11 +873,15 @@ static void launch(const GemmArgs& a, hipStream_t s) {
     const int64_t big_tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
     static const int64_t min_k = getenv("GJ_GLDS_MINK") ? atoll(getenv("GJ_GLDS_MINK")) : 384;
     const bool deep = a.K >= min_k && big_tiles >= 512;
-    v = !deep ? 1 : (sizeof(T) == 8 ? 11 : 6);
+    v = !deep ? 1 : 11;
   }
   if (v == 11) {  // LDS-DMA fp64 kernel; other dtypes / layouts / alignments take the next best tile
     if constexpr (sizeof(T) == 8 && AL == 1 && MODE != MODE_RESID) {
       if (glds_ok(a)) return launch_glds<MODE>(a, s);
+    }
+    if constexpr (sizeof(T) == 4 && AL == 1 && MODE != MODE_RESID) {
+      static const bool off = getenv("GJ_GLDS32") && atoi(getenv("GJ_GLDS32")) < 0;
+      if (!off && glds32_ok(a)) return launch_glds32<MODE>(a, s);
     }
     v = sizeof(T) == 8 ? 9 : 6;
   }
