@@ -8,7 +8,7 @@ out=gpurun_out/pmc_$tag
 mkdir -p "$out"
 timeout -k 10 120 python3 bench/gemm_probe.py "$@" > "$out/plain.json" 2>/dev/null || exit $?
 i=0
-for ctrs in "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU_MFMA_MOPS_F64" \
+for ctrs in "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES ${MOPS:-SQ_INSTS_VALU_MFMA_MOPS_F64}" \
             "SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU" \
             "FETCH_SIZE SQ_WAVE_CYCLES SQ_WAIT_ANY"; do
   i=$((i+1))

@@ -156,6 +156,28 @@ def test_gemm_variants_elimination_extras(native, variant, M, N, K, dtype):
         native.set_gemm_variant("auto")
 
 
+@pytest.mark.parametrize("M,N,K", [(2948, 2900, 520), (2950, 2900, 520), (2948, 2902, 1000)])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_gemm_deep_auto_dispatch(native, M, N, K, dtype):
+    """Deep updates with enough tiles take the LDS-DMA kernels under "auto" (fp32: the 32x32x2 one
+    when M, N are multiples of 4, else the register-staged tile): ragged edges, zero extras."""
+    native.set_gemm_variant("auto")
+    A = _rand((M, K), torch.float64, 21)
+    B = _rand((K, N), torch.float64, 22)
+    C = _rand((M, N), torch.float64, 23)
+    z0, z1, zr, zh = 128, 256, [0, 1000], 128
+    Cin = C.clone()
+    Cin[:, z0:z1] = 0
+    for r in zr:
+        Cin[r:r + zh] = 0
+    ref = Cin + A @ B
+    tol = (1e-12 if dtype == torch.float64 else 2e-5) * K
+    Cd = C.to(dtype).cuda()
+    ops.gemm(A.t().contiguous().to(dtype).cuda(), B.to(dtype).cuda(), Cd, op="acc", a_kmajor=True,
+             zero_cols=(z0, z1), zero_rows=zr, zero_row_height=zh)
+    assert (Cd.cpu().double() - ref).abs().max().item() < tol
+
+
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("count", [1, 3, 4, 6])
 def test_gemm_batch_mixed_store_acc(dtype, count):
