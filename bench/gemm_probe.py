@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--variant", default=None)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--check", action="store_true", help="compare one call against torch fp64")
+    ap.add_argument("--op", default="acc", choices=["acc", "store"], help="C += A B or C = A B")
     a = ap.parse_args()
     M, N, K = a.shape
     C_ = load_native()
@@ -41,14 +42,14 @@ def main():
         ref = C0.double() + At.double().t() @ B.double()
         err = float((C.double() - ref).abs().max() / ref.abs().max())
         del C0, ref
-    ops.gemm(At, B, C, op="acc", a_kmajor=True)
+    ops.gemm(At, B, C, op=a.op, a_kmajor=True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.reps):
-        ops.gemm(At, B, C, op="acc", a_kmajor=True)
+        ops.gemm(At, B, C, op=a.op, a_kmajor=True)
     torch.cuda.synchronize()
     dt_s = (time.perf_counter() - t0) / a.reps
-    print(json.dumps({"M": M, "N": N, "K": K, "dtype": a.dtype, "variant": a.variant or "default",
+    print(json.dumps({"M": M, "N": N, "K": K, "dtype": a.dtype, "variant": a.variant or "default", "op": a.op,
                       "ms": round(dt_s * 1e3, 4), "tflops": round(2.0 * M * N * K / dt_s / 1e12, 2), "rel_err": err}), flush=True)
 
 

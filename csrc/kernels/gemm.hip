@@ -617,6 +617,206 @@ static bool glds_ok(const GemmArgs& a) {
          a.lda * a.K * 8 < kRecords && a.ldb * a.K * 8 < kRecords && a.ldc * 128 * 8 < kRecords;
 }
 
+// ---- fp64 trailing update with the A operand straight to VGPRs (GJ_GEMM_VARIANT=dtva).
+//
+// 128 x 128 tile, 4 waves of 32 x 128.  A wave's 32 tile rows are its own, so its A fragments go
+// global -> VGPR (one 16-byte load per lane per 4-deep k step, issued PG slices ahead) and never
+// touch LDS; only B (16 x 128 per slice, read by all four waves) goes through a 2-stage LDS-DMA
+// ring, 4 one-KiB pieces per wave per slice.  A 16-byte A load gives a lane two consecutive tile
+// rows of one k, so MFMA row tile t holds tile rows 32 w + 2 i + t (i = the instruction's row);
+// the C map follows that permutation.  Per 16-deep slice a wave issues 64 MFMAs, 32 ds_read_b64
+// (0.5 per MFMA; 0.75 in the 128 x 64 kernel) and meets one barrier.  ~200 VGPRs: 2 per CU.
+// B image as in gemm_glds_f64: row k at [k][128], the 128-B halves of odd rows swapped.
+namespace dtva {
+constexpr int BM = 128, BN = 128, BK = 16, NT = 256;
+constexpr int SB = BK * BN;  // doubles per B stage
+}  // namespace dtva
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// s_waitcnt vmcnt(n) for n in {0, 4, 8, 12} (rounded down: waiting for more is always safe)
+__device__ __forceinline__ void vm_wait4(int n) {
+  if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int MODE, int PG>
+__global__ __launch_bounds__(dtva::NT, 2) void gemm_dtva_f64(GemmArgs g) {
+  using namespace dtva;
+  using MF = Mfma<double>;
+  using acc_t = MF::acc_t;
+  static_assert(PG == 1 || PG == 2, "A slices in flight");
+  constexpr int ES = 8, NJ = BN / 16, NA = PG + 1;
+  __shared__ double lds[2 * SB];
+
+  const int nwg = g.tiles_m * g.tiles_n;
+  const int tile = xcd_remap((int)blockIdx.x, nwg);
+  const int G = g.group > 0 ? g.group : 1;
+  const int grp = tile / (G * g.tiles_n), gr0 = grp * G;
+  const int gsz = (g.tiles_m - gr0) < G ? (g.tiles_m - gr0) : G;
+  const int rem = tile - grp * G * g.tiles_n;
+  const int tm = gr0 + rem % gsz, tn = rem / gsz;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const double* A = static_cast<const double*>(g.A);
+  const double* B = static_cast<const double*>(g.B);
+  double* C = static_cast<double*>(g.C);
+  const int ldc = (int)g.ldc, ldb = (int)g.ldb, lda = (int)g.lda;
+  const int cl = lane & 15;
+
+  const int Mt = (int)((g.M - m0) < BM ? (g.M - m0) : BM);
+  const int Nt = (int)((g.N - n0) < BN ? (g.N - n0) : BN);
+  const int64_t zlo = g.zc0 - n0, zhi = g.zc1 - n0;
+  const int z0 = (int)(zlo < 0 ? 0 : (zlo > BN ? BN : zlo)), z1 = (int)(zhi < 0 ? 0 : (zhi > BN ? BN : zhi));
+  int zr0[GemmExtra::kMaxZeroRows], zr1[GemmExtra::kMaxZeroRows];
+#pragma unroll
+  for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) {
+    const int64_t lo = g.zr[z] - m0, hi = g.zr[z] + g.zh - m0;
+    zr0[z] = (int)(lo < 0 ? 0 : (lo > BM ? BM : lo));
+    zr1[z] = (int)(hi < 0 ? 0 : (hi > BM ? BM : hi));
+  }
+  // accumulator (t, j, q) of lane l: tile row rbase + 8 q + t, column 16 j + (l & 15)
+  __amdgpu_buffer_rsrc_t rc = rsrc(C + m0 * g.ldc + n0);
+  const int rbase = 32 * wid + 2 * (lane >> 4);
+  const int cvoff = (rbase * ldc + cl) * ES;
+  acc_t acc[2][NJ];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = rbase + 8 * q + t;
+      const int soff = (8 * q + t) * ldc * ES;
+      bool zrow = false;
+#pragma unroll
+      for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) zrow |= (r >= zr0[z] && r < zr1[z]);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int c = cl + 16 * j;
+        if (MODE == MODE_ACC) {
+          const bool ok = r < Mt && c < Nt && !zrow && !(c >= z0 && c < z1);
+          acc[t][j][q] = bload<double>(rc, ok ? cvoff + j * 16 * ES : kOOB, soff);
+        } else {
+          acc[t][j][q] = 0.0;
+        }
+      }
+    }
+  // C must have landed before the first LDS-DMA is counted by the hand-written waits below
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) asm volatile("" ::"v"(acc[t][j][q]));
+
+  const int Kd = (int)g.K;
+  // A: lane l -> k row (l >> 4) of each 4-deep step, tile rows 32 w + 2 (l & 15) + {0, 1}
+  const int arow = 32 * wid + 2 * cl;
+  const bool a_ok = (m0 + arow) < g.M;  // M even: both rows or neither
+  __amdgpu_buffer_rsrc_t ra = rsrc(A + m0);
+  const int avoff = ((lane >> 4) * lda + arow) * ES;
+  // B: wave w moves slice rows w + 4 h; lane l -> LDS doubles 2 l, 2 l + 1 of the row
+  __amdgpu_buffer_rsrc_t rb = rsrc(B + n0);
+  const int bcol = (2 * lane) ^ ((wid & 1) * 16);
+  const bool b_ok = (n0 + bcol) < g.N;
+
+  u32x4 areg[NA][4];
+  auto issueA = [&](int kt, u32x4(&dst)[4]) {
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bool ok = a_ok && (k0 + 4 * ks + (lane >> 4)) < Kd;
+      dst[ks] = __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? avoff : kOOB, (k0 + 4 * ks) * lda * ES, 0);
+    }
+  };
+  auto issueB = [&](int kt) {
+    double* st = lds + (kt & 1) * SB;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const int kr = wid + 4 * h;
+      const bool ok = b_ok && (k0 + kr) < Kd;
+      dma16(rb, st + kr * BN, ok ? ((k0 + kr) * ldb + bcol) * ES : kOOB);
+    }
+  };
+  auto compute = [&](int kt, const u32x4(&a)[4]) {
+    const double* sb = lds + (kt & 1) * SB;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int kr = 4 * ks + (lane >> 4);
+      const int sw = (kr & 1) * 16;
+      double b[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) b[j] = sb[kr * BN + ((16 * j + cl) ^ sw)];
+      const double a0 = __builtin_bit_cast(double, u32x2{a[ks][0], a[ks][1]});
+      const double a1 = __builtin_bit_cast(double, u32x2{a[ks][2], a[ks][3]});
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        acc[0][j] = MF::op(a0, b[j], acc[0][j]);
+        acc[1][j] = MF::op(a1, b[j], acc[1][j]);
+      }
+    }
+  };
+
+  const int nk = (int)((g.K + BK - 1) / BK);
+  // issue order: B(0), A(0) .. A(PG-1); then body kt issues B(kt+1), A(kt+PG)
+  issueB(0);
+  issueA(0, areg[0]);
+  if (PG == 2 && nk > 1) issueA(1, areg[1]);
+  vm_wait4(4 * ((PG == 2 && nk > 1) ? 2 : 1));  // B(0) landed (A is waited for by the compiler)
+  __builtin_amdgcn_s_barrier();
+  auto body = [&](auto P, int kt) {
+    constexpr int p = decltype(P)::value;
+    const bool nb = kt + 1 < nk, na = kt + PG < nk;
+    if (nb) issueB(kt + 1);
+    if (na) issueA(kt + PG, areg[(p + PG) % NA]);
+    compute(kt, areg[p]);
+    if (nb) {
+      vm_wait4(na ? 4 : 0);  // B(kt+1) landed; A(kt+PG) may stay in flight
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  };
+  int kt = 0;
+  for (; kt + NA <= nk; kt += NA) {
+    body(std::integral_constant<int, 0>{}, kt);
+    body(std::integral_constant<int, 1>{}, kt + 1);
+    if constexpr (NA == 3) body(std::integral_constant<int, 2>{}, kt + 2);
+  }
+  if (kt < nk) body(std::integral_constant<int, 0>{}, kt);
+  if (kt + 1 < nk) body(std::integral_constant<int, 1>{}, kt + 1);
+
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = rbase + 8 * q + t;
+      const int soff = (8 * q + t) * ldc * ES;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int c = cl + 16 * j;
+        bstore(acc[t][j][q], rc, (r < Mt && c < Nt) ? cvoff + j * 16 * ES : kOOB, soff);
+      }
+    }
+}
+
+template <int MODE>
+static void launch_dtva(const GemmArgs& a0, hipStream_t s) {
+  GemmArgs a = a0;
+  a.tiles_m = (int)((a.M + dtva::BM - 1) / dtva::BM);
+  a.tiles_n = (int)((a.N + dtva::BN - 1) / dtva::BN);
+  const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;
+  if (nwg <= 0) return;
+  static const int pg = getenv("GJ_DTVA_PG") ? atoi(getenv("GJ_DTVA_PG")) : 2;
+  static const int group = getenv("GJ_GEMM_GROUP") ? atoi(getenv("GJ_GEMM_GROUP")) : 4;
+  a.group = group;
+  const dim3 grid((unsigned)nwg), blk(dtva::NT);
+  if (pg == 1) hipLaunchKernelGGL((gemm_dtva_f64<MODE, 1>), grid, blk, 0, s, a);
+  else hipLaunchKernelGGL((gemm_dtva_f64<MODE, 2>), grid, blk, 0, s, a);
+}
+
 // ---- fp32 trailing-update GEMM: the same LDS-DMA ring, built around v_mfma_f32_32x32x2_f32.
 //
 // The 32 x 32 x 2 instruction does the work of two 16 x 16 x 4 ones for the same two operand
@@ -848,7 +1048,7 @@ static int gemm_variant() {
 }
 int gemm_variant_id(const char* name) {
   const std::string s(name);
-  static const char* names[] = {"big", "narrow", "", "", "", "", "squarepf", "", "", "bigpf", "auto", "glds"};
+  static const char* names[] = {"big", "narrow", "", "", "", "", "squarepf", "", "", "bigpf", "auto", "glds", "dtva"};
   for (int i = 0; i < (int)(sizeof(names) / sizeof(names[0])); ++i)
     if (*names[i] && s == names[i]) return i;
   return kAutoVariant;
@@ -873,7 +1073,14 @@ static void launch(const GemmArgs& a, hipStream_t s) {
     const int64_t big_tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
     static const int64_t min_k = getenv("GJ_GLDS_MINK") ? atoll(getenv("GJ_GLDS_MINK")) : 384;
     const bool deep = a.K >= min_k && big_tiles >= 512;
-    v = !deep ? 1 : 11;
+    static const bool deep_dtva = getenv("GJ_DEEP_DTVA") && atoi(getenv("GJ_DEEP_DTVA")) > 0;
+    v = !deep ? 1 : (deep_dtva ? 12 : 11);
+  }
+  if (v == 12) {  // A-direct fp64 kernel (candidate); anything it cannot take goes the auto way
+    if constexpr (sizeof(T) == 8 && AL == 1 && MODE != MODE_RESID) {
+      if (glds_ok(a)) return launch_dtva<MODE>(a, s);
+    }
+    v = 11;
   }
   if (v == 11) {  // LDS-DMA fp64 kernel; other dtypes / layouts / alignments take the next best tile
     if constexpr (sizeof(T) == 8 && AL == 1 && MODE != MODE_RESID) {

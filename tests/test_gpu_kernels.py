@@ -124,7 +124,7 @@ def test_row_abs_max_and_residual():
     assert r < 1e-10 and abs(r - ref) < 1e-11
 
 
-GEMM_VARIANTS = ["big", "narrow", "squarepf", "bigpf", "auto", "glds"]
+GEMM_VARIANTS = ["big", "narrow", "squarepf", "bigpf", "auto", "glds", "dtva"]
 
 
 @pytest.mark.parametrize("variant", GEMM_VARIANTS)
@@ -158,10 +158,12 @@ def test_gemm_variants_elimination_extras(native, variant, M, N, K, dtype):
 
 @pytest.mark.parametrize("M,N,K", [(2948, 2900, 520), (2950, 2900, 520), (2948, 2902, 1000)])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
-def test_gemm_deep_auto_dispatch(native, M, N, K, dtype):
+@pytest.mark.parametrize("variant", ["auto", "dtva"])
+def test_gemm_deep_auto_dispatch(native, M, N, K, dtype, variant):
     """Deep updates with enough tiles take the LDS-DMA kernels under "auto" (fp32: the 32x32x2 one
-    when M, N are multiples of 4, else the register-staged tile): ragged edges, zero extras."""
-    native.set_gemm_variant("auto")
+    when M, N are multiples of 4, else the register-staged tile), or the A-direct fp64 kernel
+    under "dtva": ragged edges, zero extras."""
+    native.set_gemm_variant(variant)
     A = _rand((M, K), torch.float64, 21)
     B = _rand((K, N), torch.float64, 22)
     C = _rand((M, N), torch.float64, 23)
@@ -173,8 +175,11 @@ def test_gemm_deep_auto_dispatch(native, M, N, K, dtype):
     ref = Cin + A @ B
     tol = (1e-12 if dtype == torch.float64 else 2e-5) * K
     Cd = C.to(dtype).cuda()
-    ops.gemm(A.t().contiguous().to(dtype).cuda(), B.to(dtype).cuda(), Cd, op="acc", a_kmajor=True,
-             zero_cols=(z0, z1), zero_rows=zr, zero_row_height=zh)
+    try:
+        ops.gemm(A.t().contiguous().to(dtype).cuda(), B.to(dtype).cuda(), Cd, op="acc", a_kmajor=True,
+                 zero_cols=(z0, z1), zero_rows=zr, zero_row_height=zh)
+    finally:
+        native.set_gemm_variant("auto")
     assert (Cd.cpu().double() - ref).abs().max().item() < tol
 
 
