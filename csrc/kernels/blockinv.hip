@@ -652,8 +652,341 @@ __global__ __launch_bounds__(256) void block_inverse_generic(const T* __restrict
   }
 }
 
+// Panel-blocked sweep for the large blocks (256 < m <= 1024, fp64 and fp32): reference
+// inverse_block (main.cpp:746-820) + block_norm (main.cpp:669-683), same pivot rule as the
+// matrix-core kernels (largest magnitude, ties to the lowest current position under the
+// reference's row swaps).  256 threads; thread tid owns block rows tid + 256 s (s < RPT).
+//  * The working block lives column-major in a global (L2-resident) scratch slab, so every pass
+//    over it is coalesced (threads = consecutive rows).
+//  * A panel of PB columns is factored in REGISTERS (each thread its rows x PB): per step a
+//    block-wide exact argmax (wave butterfly on (magnitude bits, position), 4 partials in LDS), the
+//    pivot row broadcast through LDS, and the rank-1 update of the thread's own panel rows — two
+//    barriers per step, no global traffic.
+//  * The rest of the block then takes the panel as ONE rank-PB update, X += U R (U = the panel's
+//    multipliers, still in the owners' registers; R = the PB pivot rows before the panel, staged in
+//    LDS as [column][PB] so every thread reads the same column: broadcast), i.e. one read-modify-
+//    write pass over the block per PB steps instead of per step, and the panel's own columns
+//    become U + E (same panel algebra as blockinv_mfma.hip).
+// Replaces the per-step global sweep (block_inverse_generic, kept for m > 1024).
+// Branch-free buffer access for the blocked kernel: a masked lane passes an out-of-range offset
+// (load returns 0, store is dropped) — a per-lane branch around a load makes the compiler drain
+// vmcnt at the merge, which serialises the batched loads below.
+constexpr int kBbRecords = 0x7ffffff0, kBbOOB = 0x7ffffff8;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bb_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, kBbRecords, 0x00020000);
+}
+template <typename T>
+__device__ __forceinline__ T bb_load(__amdgpu_buffer_rsrc_t r, int off) {
+  if constexpr (sizeof(T) == 8) {
+    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(T, (u2)__builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+  } else {
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+  }
+}
+template <typename T>
+__device__ __forceinline__ void bb_store(T v, __amdgpu_buffer_rsrc_t r, int off) {
+  if constexpr (sizeof(T) == 8) {
+    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, off, 0, 0);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, off, 0, 0);
+  }
+}
+
+template <typename T, int RPT, int PB>
+__global__ __launch_bounds__(256) void block_inverse_blocked(const T* __restrict__ Lt, int64_t ldl,
+                                                             T* __restrict__ inv_t, double* __restrict__ scores,
+                                                             int32_t* __restrict__ valid,
+                                                             const int32_t* __restrict__ used, int m, int64_t p,
+                                                             int64_t k, double thresh, T* __restrict__ scratch,
+                                                             int32_t* __restrict__ piv_out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char bb_smem[];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (used[(int64_t)b * p + k]) {
+    if (tid == 0) {
+      valid[b] = 0;
+      scores[b] = 0.0;
+    }
+    return;
+  }
+  T* R = reinterpret_cast<T*>(bb_smem);                 // [m][PB]: pivot rows before the panel
+  int* pos = reinterpret_cast<int*>(R + (size_t)m * PB);  // current position of every row
+  int* posrow = pos + m;                                  // row at every position
+  int* prow = posrow + m;                                 // prow[c] = pivot row of column c
+  int* kinv = prow + m;                                   // kinv[r] = column pivoted on row r
+  __shared__ T rowb[PB];
+  __shared__ int rsel[PB];
+  __shared__ unsigned long long redk[4];
+  __shared__ int redp[4], redr[4];
+  __shared__ double redn[4];
+
+  T* Wc = scratch + (int64_t)b * m * m;  // column-major: Wc[j * m + i] = W[i][j]
+  constexpr int ES = (int)sizeof(T);
+  const __amdgpu_buffer_rsrc_t rw = bb_rsrc(Wc), rl = bb_rsrc(Lt + (int64_t)b * m);
+  auto woff = [&](int j, int i, bool ok) { return ok ? (j * m + i) * ES : kBbOOB; };
+  // every loop over the block below keeps JB independent loads in flight per thread (one wave per
+  // SIMD: a load-use chain per element would leave the loop latency-bound)
+  constexpr int JB = 8;
+  for (int j0 = 0; j0 < m; j0 += JB) {
+    T x[JB][RPT];
+#pragma unroll
+    for (int jb = 0; jb < JB; ++jb)
+#pragma unroll
+      for (int s = 0; s < RPT; ++s) {
+        const int i = tid + 256 * s, j = j0 + jb;
+        x[jb][s] = bb_load<T>(rl, (i < m && j < m) ? (int)(((int64_t)j * ldl + i) * ES) : kBbOOB);
+      }
+#pragma unroll
+    for (int jb = 0; jb < JB; ++jb)
+#pragma unroll
+      for (int s = 0; s < RPT; ++s) {
+        const int i = tid + 256 * s, j = j0 + jb;
+        bb_store<T>(-x[jb][s], rw, woff(j, i, i < m && j < m));
+      }
+  }
+  for (int i = tid; i < m; i += 256) {
+    pos[i] = i;
+    posrow[i] = i;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+
+  bool mine_used[RPT];
+#pragma unroll
+  for (int s = 0; s < RPT; ++s) mine_used[s] = (tid + 256 * s >= m);
+  bool sing = false;
+  for (int c0 = 0; c0 < m && !sing; c0 += PB) {
+    const int pb = min(PB, m - c0);
+    T P[RPT][PB];
+#pragma unroll
+    for (int s = 0; s < RPT; ++s) {
+      const int i = tid + 256 * s;
+#pragma unroll
+      for (int kk = 0; kk < PB; ++kk) P[s][kk] = bb_load<T>(rw, woff(c0 + kk, i, i < m && kk < pb));
+    }
+#pragma unroll
+    for (int jj = 0; jj < PB; ++jj) {
+      if (jj >= pb || sing) break;
+      // block-wide argmax of |column jj| over the unused rows: larger magnitude, then lower position
+      unsigned long long bk = 0;
+      int bp = 0x7fffffff, br = -1;
+#pragma unroll
+      for (int s = 0; s < RPT; ++s) {
+        const int i = tid + 256 * s;
+        if (mine_used[s]) continue;
+        const unsigned long long key =
+            __builtin_bit_cast(unsigned long long, (double)P[s][jj]) & 0x7FFFFFFFFFFFFFFFull;
+        const int ps = pos[i];
+        if (br < 0 || key > bk || (key == bk && ps < bp)) {
+          bk = key;
+          bp = ps;
+          br = i;
+        }
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        const unsigned long long ok = __shfl_xor(bk, o, 64);
+        const int op = __shfl_xor(bp, o, 64), orr = __shfl_xor(br, o, 64);
+        if (orr >= 0 && (br < 0 || ok > bk || (ok == bk && op < bp))) {
+          bk = ok;
+          bp = op;
+          br = orr;
+        }
+      }
+      if (lane == 0) {
+        redk[wave] = bk;
+        redp[wave] = bp;
+        redr[wave] = br;
+      }
+      __syncthreads();  // B1: partials published (and every read of pos / rowb of the last step done)
+      int r = -1;
+      {
+        unsigned long long fk = 0;
+        int fp = 0x7fffffff;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const int wr = redr[w];
+          if (wr >= 0 && (r < 0 || redk[w] > fk || (redk[w] == fk && redp[w] < fp))) {
+            fk = redk[w];
+            fp = redp[w];
+            r = wr;
+          }
+        }
+      }
+      if (r < 0) r = c0 + jj;  // no free row (cannot happen for jj < m): any row, singular below
+      if (tid == (r & 255)) {
+#pragma unroll
+        for (int s = 0; s < RPT; ++s)
+          if ((r >> 8) == s) {
+#pragma unroll
+            for (int kk = 0; kk < PB; ++kk) rowb[kk] = P[s][kk];
+          }
+      }
+      if (tid == 0) {  // the reference's swap of step c0 + jj: pivot row <-> row at that position
+        const int kp = c0 + jj, r2 = posrow[kp], pr = pos[r];
+        pos[r2] = pr;
+        posrow[pr] = r2;
+        pos[r] = kp;
+        posrow[kp] = r;
+        prow[kp] = r;
+        kinv[r] = kp;
+        rsel[jj] = r;
+      }
+      __syncthreads();  // B2: pivot row and book-keeping published
+      T rv[PB];
+#pragma unroll
+      for (int kk = 0; kk < PB; ++kk) rv[kk] = rowb[kk];
+      const T piv = rv[jj];
+      if (!(fabs((double)piv) >= thresh)) {
+        sing = true;  // every thread read the same pivot: a uniform exit
+        break;
+      }
+      const T inv = fast_recip(piv);
+#pragma unroll
+      for (int s = 0; s < RPT; ++s) {
+        const int i = tid + 256 * s;
+        const T u = (i == r) ? inv - T(1) : -P[s][jj] * inv;
+#pragma unroll
+        for (int kk = 0; kk < PB; ++kk)
+          if (kk != jj) P[s][kk] = __builtin_fma(u, rv[kk], P[s][kk]);
+        P[s][jj] = u;
+        if (i == r) mine_used[s] = true;
+      }
+    }
+    if (sing) break;
+    // R = the panel's pivot rows over every column, before the panel (Wc is still untouched)
+    for (int j = tid; j < m; j += 256)
+#pragma unroll
+      for (int kk = 0; kk < PB; ++kk) R[j * PB + kk] = bb_load<T>(rw, woff(j, rsel[kk < pb ? kk : 0], kk < pb));
+    __syncthreads();  // B3: R staged; every thread is done reading Wc for this panel
+    // X += U R outside the panel (own rows, every column); the panel's columns := U + E
+    for (int j0 = 0; j0 < m; j0 += JB) {
+      T x[JB][RPT];
+#pragma unroll
+      for (int jb = 0; jb < JB; ++jb)
+#pragma unroll
+        for (int s = 0; s < RPT; ++s) {
+          const int i = tid + 256 * s, j = j0 + jb;
+          x[jb][s] = bb_load<T>(rw, woff(j, i, i < m && j < m));
+        }
+#pragma unroll
+      for (int jb = 0; jb < JB; ++jb) {
+        const int j = j0 + jb;
+        if (j >= m || (j >= c0 && j < c0 + pb)) continue;  // uniform
+        T rj[PB];
+#pragma unroll
+        for (int kk = 0; kk < PB; ++kk) rj[kk] = R[j * PB + kk];
+#pragma unroll
+        for (int s = 0; s < RPT; ++s) {
+          const int i = tid + 256 * s;
+          T v = x[jb][s];
+#pragma unroll
+          for (int kk = 0; kk < PB; ++kk) v = __builtin_fma(P[s][kk], rj[kk], v);
+          bb_store<T>(v, rw, woff(j, i, i < m));
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < RPT; ++s) {
+      const int i = tid + 256 * s;
+#pragma unroll
+      for (int kk = 0; kk < PB; ++kk)
+        bb_store<T>(P[s][kk] + (i == rsel[kk < pb ? kk : 0] ? T(1) : T(0)), rw, woff(c0 + kk, i, i < m && kk < pb));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();  // B4: the block is consistent again (the next R reads other threads' rows)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+  if (sing) {
+    if (tid == 0) {
+      valid[b] = 0;
+      scores[b] = 0.0;
+    }
+    return;
+  }
+  if (piv_out)  // test probe: the pivot row of every column
+    for (int c = tid; c < m; c += 256) piv_out[(int64_t)b * m + c] = prow[c];
+  // inverse, transposed: inv(W)[kinv[i]][prow[u]] = W_swept[i][u] -> inv_t[prow[u]][kinv[i]]; the
+  // row abs-sums of W_swept are those of the inverse (block_norm)
+  const __amdgpu_buffer_rsrc_t ro = bb_rsrc(inv_t + (int64_t)b * m * m);
+  double rs[RPT];
+#pragma unroll
+  for (int s = 0; s < RPT; ++s) rs[s] = 0.0;
+  int ki[RPT];
+#pragma unroll
+  for (int s = 0; s < RPT; ++s) ki[s] = (tid + 256 * s < m) ? kinv[tid + 256 * s] : 0;
+  for (int u0 = 0; u0 < m; u0 += JB) {
+    T x[JB][RPT];
+#pragma unroll
+    for (int ub = 0; ub < JB; ++ub)
+#pragma unroll
+      for (int s = 0; s < RPT; ++s) {
+        const int i = tid + 256 * s, u = u0 + ub;
+        x[ub][s] = bb_load<T>(rw, woff(u, i, i < m && u < m));
+      }
+#pragma unroll
+    for (int ub = 0; ub < JB; ++ub) {
+      const int u = u0 + ub;
+      if (u >= m) continue;
+      const int o = prow[u] * m;
+#pragma unroll
+      for (int s = 0; s < RPT; ++s) {
+        const bool ok = tid + 256 * s < m;
+        bb_store<T>(x[ub][s], ro, ok ? (o + ki[s]) * ES : kBbOOB);
+        rs[s] += fabs((double)x[ub][s]);  // masked lanes hold 0
+      }
+    }
+  }
+  double mx = 0.0;
+#pragma unroll
+  for (int s = 0; s < RPT; ++s) mx = fmax(mx, rs[s]);
+  mx = wave_max_f64(mx);
+  if (lane == 0) redn[wave] = mx;
+  __syncthreads();
+  if (tid == 0) {
+    const double sc = fmax(fmax(redn[0], redn[1]), fmax(redn[2], redn[3]));
+    scores[b] = sc;
+    valid[b] = isfinite(sc) ? 1 : 0;
+  }
+}
+
+template <typename T>
+static bool launch_blocked(const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,
+                           const int32_t* used, const Layout& L, double thresh, hipStream_t s, void* scratch) {
+  const int m = (int)L.m;
+  if (m <= 256 || m > 1024) return false;
+  const unsigned grid = (unsigned)L.nblk;
+  const int RPT = (m + 255) / 256;
+  const int PBv = RPT <= 2 ? 16 : 8;
+  const size_t lds = (size_t)m * PBv * sizeof(T) + 4 * (size_t)m * sizeof(int);
+  const T* lt = static_cast<const T*>(Lt);
+  T* it = static_cast<T*>(inv_t);
+  T* sc = static_cast<T*>(scratch);
+  int32_t* probe = block_inverse_probe();
+#define GJ_BB(RP, PBB)                                                                               \
+  do {                                                                                                \
+    static bool attr = false;                                                                         \
+    if (!attr) {                                                                                      \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&block_inverse_blocked<T, RP, PBB>),    \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);               \
+      attr = true;                                                                                    \
+    }                                                                                                 \
+    hipLaunchKernelGGL((block_inverse_blocked<T, RP, PBB>), dim3(grid), dim3(256), lds, s, lt, ldl,   \
+                       it, scores, valid, used, m, L.p, L.k, thresh, sc, probe);                      \
+  } while (0)
+  if (RPT == 2) GJ_BB(2, 16);
+  else if (RPT == 3) GJ_BB(3, 8);
+  else GJ_BB(4, 8);
+#undef GJ_BB
+  return true;
+}
+
 // 0 = matrix-core panels (default), 1 = per-step sweep, 2 = one-wave panels, 3/4 = matrix-core
-// pivot-wave forms, 5 = co-resident L2-image kernel (fp64 32 < m <= 128; GJ_BI_VARIANT=co)
+// pivot-wave forms, 5 = co-resident L2-image kernel (fp64 32 < m <= 128; GJ_BI_VARIANT=co),
+// 6 = the per-step global sweep for m > 256 instead of the panel-blocked kernel (reference timing)
 static int g_bi_variant = -1;
 static int bi_variant() {
   if (g_bi_variant < 0) {
@@ -702,6 +1035,8 @@ static void launch_bi(const void* Lt, int64_t ldl, void* inv_t, double* scores, 
   else if (m <= 256 && sizeof(T) == 4)  // 256x256 fp32 = 64 VGPRs/lane at 1024 threads
     hipLaunchKernelGGL((block_inverse_kernel<T, 256, 1024>), dim3(grid), dim3(1024), 0, s, lt, ldl,
                        it, scores, valid, used, m, L.p, L.k, thresh);
+  else if (g_bi_variant != 6 && launch_blocked<T>(Lt, ldl, inv_t, scores, valid, used, L, thresh, s, scratch))
+    return;
   else
     hipLaunchKernelGGL((block_inverse_generic<T>), dim3(grid), dim3(256), 0, s, lt, ldl, it, scores,
                        valid, used, m, L.p, L.k, thresh, static_cast<T*>(scratch), iscratch);

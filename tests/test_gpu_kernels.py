@@ -59,14 +59,14 @@ def test_extract_neg_t():
     assert torch.equal(Lt.cpu(), -X.cpu()[:, 128:224].t())
 
 
-@pytest.fixture(params=["panel", "sweep", "panel1", "co"])
+@pytest.fixture(params=["panel", "sweep", "panel1", "co", "generic"])
 def bi_variant(request, native):
     native.set_block_inverse_variant(request.param)
     yield request.param
     native.set_block_inverse_variant("panel")
 
 
-@pytest.mark.parametrize("m", [16, 37, 60, 64, 100, 128, 200, 256, 300])
+@pytest.mark.parametrize("m", [16, 37, 60, 64, 100, 128, 200, 256, 300, 512, 700, 1000])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 def test_block_inverse(m, dtype, bi_variant):
     nblk = 6
@@ -228,7 +228,9 @@ def _reference_pivots(W):
 
 
 @pytest.mark.parametrize("m,dtype", [(40, torch.float64), (128, torch.float64), (200, torch.float64),
-                                     (256, torch.float64), (40, torch.float32), (128, torch.float32)])
+                                     (256, torch.float64), (40, torch.float32), (128, torch.float32),
+                                     (300, torch.float64), (512, torch.float64), (700, torch.float32),
+                                     (1000, torch.float64)])
 def test_block_inverse_pivot_rule(native, m, dtype):
     """exact magnitudes (ties resolved in the low word of the fp64 key) and, on
     equal magnitudes, the row at the lowest CURRENT position under the reference's swaps."""
