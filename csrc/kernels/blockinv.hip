@@ -70,7 +70,7 @@ __global__ __launch_bounds__(NTH) void block_inverse_kernel(const T* __restrict_
                                                             int32_t* __restrict__ valid,
                                                             const int32_t* __restrict__ used,
                                                             int m, int64_t p, int64_t k,
-                                                            double thresh) {
+                                                            double thresh, int32_t* __restrict__ piv_out) {
   constexpr int TR = NTH / 32;   // thread rows (column groups)
   constexpr int RI = MP / 32;    // rows per thread
   constexpr int CJ = MP / TR;    // columns per thread
@@ -92,6 +92,8 @@ __global__ __launch_bounds__(NTH) void block_inverse_kernel(const T* __restrict_
   __shared__ T rowv[2][MP];
   __shared__ int prow[MP];
   __shared__ int kinv[MP];
+  __shared__ int pos[MP];     // current position of every row under the reference's swaps
+  __shared__ int posrow[MP];  // row at every position
   __shared__ double red[MP];
   __shared__ double wmax[NTH / 64];
 
@@ -106,7 +108,11 @@ __global__ __launch_bounds__(NTH) void block_inverse_kernel(const T* __restrict_
                                    : (i == j ? T(1) : T(0));
     }
   }
-  for (int i = tid; i < MP; i += NTH) red[i] = 0.0;
+  for (int i = tid; i < MP; i += NTH) {
+    red[i] = 0.0;
+    pos[i] = i;
+    posrow[i] = i;
+  }
 
   bool lused[SCAN];
 #pragma unroll
@@ -129,17 +135,35 @@ __global__ __launch_bounds__(NTH) void block_inverse_kernel(const T* __restrict_
       }
     }
     __syncthreads();
-    // (2) argmax |colv| over unused real rows, lowest row on ties (every wave, redundantly, with
-    // register-only cross-lane moves); r is wave-uniform -> scalar branches below
-    double key = -1.0;
+    // (2) argmax |colv| over unused real rows — the reference's scan exactly (main.cpp:756-763):
+    // the largest magnitude (64-bit keys), on equal magnitudes the lowest CURRENT position under
+    // its row swaps (pos); every wave redundantly, register-only butterfly; r is wave-uniform
+    uint64_t bk = 0;
+    int bp = 0x7fffffff, br = -1;
 #pragma unroll
     for (int s = 0; s < SCAN; ++s) {
       const int i = lane + 64 * s;
-      const double kv = (i < m && !lused[s]) ? pivot_key(fabs((double)colv[par][i]), i) : -1.0;
-      key = fmax(key, kv);
+      if (i < m && !lused[s]) {
+        const uint64_t key = __builtin_bit_cast(uint64_t, fabs((double)colv[par][i])) & 0x7FFFFFFFFFFFFFFFull;
+        const int ps = pos[i];
+        if (br < 0 || key > bk || (key == bk && ps < bp)) {
+          bk = key;
+          bp = ps;
+          br = i;
+        }
+      }
     }
-    key = wave_max_f64(key);
-    const int r = __builtin_amdgcn_readfirstlane(pivot_key_row(key));
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const uint64_t ok = __shfl_xor(bk, o, 64);
+      const int op = __shfl_xor(bp, o, 64), orr = __shfl_xor(br, o, 64);
+      if (orr >= 0 && (br < 0 || ok > bk || (ok == bk && op < bp))) {
+        bk = ok;
+        bp = op;
+        br = orr;
+      }
+    }
+    const int r = __builtin_amdgcn_readfirstlane(br < 0 ? kk : br);
     const T pivv = colv[par][r];
     if (!(fabs((double)pivv) >= thresh)) {  // uniform across the workgroup
       singular = true;
@@ -168,6 +192,13 @@ __global__ __launch_bounds__(NTH) void block_inverse_kernel(const T* __restrict_
         }
     }
     __syncthreads();
+    if (tid == 0) {  // the reference's swap of step kk (every wave has finished this step's scan)
+      const int r2 = posrow[kk], pr = pos[r];
+      pos[r2] = pr;
+      posrow[pr] = r2;
+      pos[r] = kk;
+      posrow[kk] = r;
+    }
     // (4) rank-1 update: column kk enters as 0 (-> -f*inv), pivot row fixed up afterwards
     if (col_owner) {
 #pragma unroll
@@ -203,6 +234,8 @@ __global__ __launch_bounds__(NTH) void block_inverse_kernel(const T* __restrict_
     return;
   }
 
+  if (piv_out)  // test probe: the pivot row of every column
+    for (int c = tid; c < m; c += NTH) piv_out[(int64_t)b * m + c] = prow[c];
   // ||inv||_inf = max row abs-sum of the swept block (row/column permutations do not change it)
 #pragma unroll
   for (int qi = 0; qi < RI; ++qi) {
@@ -1025,16 +1058,16 @@ static void launch_bi(const void* Lt, int64_t ldl, void* inv_t, double* scores, 
                        it, scores, valid, used, m, L.p, L.k, thresh);
   else if (m <= 32)
     hipLaunchKernelGGL((block_inverse_kernel<T, 32, 256>), dim3(grid), dim3(256), 0, s, lt, ldl, it,
-                       scores, valid, used, m, L.p, L.k, thresh);
+                       scores, valid, used, m, L.p, L.k, thresh, block_inverse_probe());
   else if (m <= 64)
     hipLaunchKernelGGL((block_inverse_kernel<T, 64, 256>), dim3(grid), dim3(256), 0, s, lt, ldl, it,
-                       scores, valid, used, m, L.p, L.k, thresh);
+                       scores, valid, used, m, L.p, L.k, thresh, block_inverse_probe());
   else if (m <= 128)  // 16 elements per thread, 4 waves per SIMD to hide the per-step latency chain
     hipLaunchKernelGGL((block_inverse_kernel<T, 128, 1024>), dim3(grid), dim3(1024), 0, s, lt, ldl,
-                       it, scores, valid, used, m, L.p, L.k, thresh);
+                       it, scores, valid, used, m, L.p, L.k, thresh, block_inverse_probe());
   else if (m <= 256 && sizeof(T) == 4)  // 256x256 fp32 = 64 VGPRs/lane at 1024 threads
     hipLaunchKernelGGL((block_inverse_kernel<T, 256, 1024>), dim3(grid), dim3(1024), 0, s, lt, ldl,
-                       it, scores, valid, used, m, L.p, L.k, thresh);
+                       it, scores, valid, used, m, L.p, L.k, thresh, block_inverse_probe());
   else if (g_bi_variant != 6 && launch_blocked<T>(Lt, ldl, inv_t, scores, valid, used, L, thresh, s, scratch))
     return;
   else

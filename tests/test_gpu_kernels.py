@@ -227,13 +227,19 @@ def _reference_pivots(W):
     return piv
 
 
-@pytest.mark.parametrize("m,dtype", [(40, torch.float64), (128, torch.float64), (200, torch.float64),
-                                     (256, torch.float64), (40, torch.float32), (128, torch.float32),
-                                     (300, torch.float64), (512, torch.float64), (700, torch.float32),
-                                     (1000, torch.float64)])
-def test_block_inverse_pivot_rule(native, m, dtype):
+@pytest.mark.parametrize("m,dtype,variant", [
+    (40, torch.float64, "panel"), (128, torch.float64, "panel"), (200, torch.float64, "panel"),
+    (256, torch.float64, "panel"), (40, torch.float32, "panel"), (128, torch.float32, "panel"),
+    (300, torch.float64, "panel"), (512, torch.float64, "panel"), (700, torch.float32, "panel"),
+    (1000, torch.float64, "panel"),
+    # the register sweep kernel: default for m <= 16 and fp32 128 < m <= 256, variant "sweep" else
+    (16, torch.float64, "panel"), (200, torch.float32, "panel"), (128, torch.float64, "sweep"),
+    (60, torch.float32, "sweep")])
+def test_block_inverse_pivot_rule(native, m, dtype, variant):
     """exact magnitudes (ties resolved in the low word of the fp64 key) and, on
-    equal magnitudes, the row at the lowest CURRENT position under the reference's swaps."""
+    equal magnitudes, the row at the lowest CURRENT position under the reference's swaps — in
+    every candidate-inverse kernel."""
+    native.set_block_inverse_variant(variant)
     rng = np.random.default_rng(7 + m)
     eps = 2.0 ** -51 if dtype == torch.float64 else 2.0 ** -22
     Ws = []
@@ -261,6 +267,7 @@ def test_block_inverse_pivot_rule(native, m, dtype):
         torch.cuda.synchronize()
     finally:
         native.set_block_inverse_probe(0)
+        native.set_block_inverse_variant("panel")
     assert valid.cpu().tolist() == [1] * nblk
     got = probe.cpu().numpy().reshape(nblk, m)
     assert got[0][0] == 5 and got[0][1] == 3
