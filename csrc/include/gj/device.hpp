@@ -134,6 +134,10 @@ class Device {
   virtual void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                              int32_t* valid, const int32_t* used, const Layout& L, double thresh,
                              int s) = 0;
+  // Kernel family for the following block_inverse calls (-1 = the process default; 5 = the
+  // co-resident form, which the engine picks where its pivot chain waits for whole CUs).  Devices
+  // with a single implementation ignore it.
+  virtual void set_block_inverse_hint(int variant) { (void)variant; }
   // Local argmin over this rank's candidates -> *out.
   virtual void pivot_local(const double* scores, const int32_t* valid, const int32_t* used,
                            const int32_t* pos, const Layout& L, PivotRec* out, int s) = 0;

@@ -196,6 +196,7 @@ class Engine {
   int d_ = 1;
   std::string bcast_algo_ = "ring";
   bool comm_small_tiles_ = false;  // COMM chunk-normalisation GEMMs on the small latency tile
+  int bi_hint_ = -1;               // candidate-inverse kernel family (Device::set_block_inverse_hint)
   double norm_a_ = -1;
 
   // chunk plan (block-column ranges, multiples of d_ blocks so a panel never straddles chunks)

@@ -57,6 +57,7 @@ class HipDevice : public Device {
   void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                      int32_t* valid, const int32_t* used, const Layout& L, double thresh,
                      int s) override;
+  void set_block_inverse_hint(int variant) override { bi_hint_ = variant; }
   void pivot_local(const double* scores, const int32_t* valid, const int32_t* used,
                    const int32_t* pos, const Layout& L, PivotRec* out, int s) override;
   void pivot_select_single(const double* scores, const int32_t* valid, const Layout& L, int32_t t,
@@ -88,6 +89,7 @@ class HipDevice : public Device {
 
   int dev_ = 0;
   void* streams_[kNumStreams] = {};
+  int bi_hint_ = -1;  // set_block_inverse_hint
   std::vector<void*> events_;
   void* scratch_[2] = {nullptr, nullptr};
   size_t scratch_sz_[2] = {0, 0};

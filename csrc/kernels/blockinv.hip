@@ -1034,12 +1034,12 @@ int block_inverse_variant() { return bi_variant(); }
 template <typename T>
 static void launch_bi(const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,
                       const int32_t* used, const Layout& L, double thresh, hipStream_t s,
-                      void* scratch, int* iscratch) {
+                      void* scratch, int* iscratch, int variant) {
   const int m = (int)L.m;
   const unsigned grid = (unsigned)L.nblk;
   const T* lt = static_cast<const T*>(Lt);
   T* it = static_cast<T*>(inv_t);
-  const int g_bi_variant = bi_variant();
+  const int g_bi_variant = variant >= 0 ? variant : bi_variant();
   if (g_bi_variant == 5 && block_inverse_co(sizeof(T) == 8 ? DType::F64 : DType::F32, Lt, ldl, inv_t, scores,
                                             valid, used, L, thresh, s, scratch))
     return;
@@ -1077,8 +1077,9 @@ static void launch_bi(const void* Lt, int64_t ldl, void* inv_t, double* scores, 
 
 static bool generic_path(DType dt, int64_t m) { return dt == DType::F64 ? m > 128 : m > 256; }
 
-size_t block_inverse_scratch_bytes(DType dt, const Layout& L) {
-  if (bi_variant() == 5 && dt == DType::F64 && L.m > 32 && L.m <= 128) return block_inverse_big_scratch_bytes(dt, L);
+size_t block_inverse_scratch_bytes(DType dt, const Layout& L, int variant) {
+  const int v = variant >= 0 ? variant : bi_variant();
+  if (v == 5 && dt == DType::F64 && L.m > 32 && L.m <= 128) return block_inverse_big_scratch_bytes(dt, L);
   if (!generic_path(dt, L.m)) return 0;
   if (const size_t big = block_inverse_big_scratch_bytes(dt, L)) return big;
   return (size_t)L.nblk * L.m * L.m * dtype_size(dt);
@@ -1089,12 +1090,12 @@ size_t block_inverse_iscratch_bytes(const Layout& L) {
 
 void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                    int32_t* valid, const int32_t* used, const Layout& L, double thresh,
-                   hipStream_t s, void* scratch, int* iscratch) {
+                   hipStream_t s, void* scratch, int* iscratch, int variant) {
   if (L.nblk <= 0) return;
   if (dt == DType::F64)
-    launch_bi<double>(Lt, ldl, inv_t, scores, valid, used, L, thresh, s, scratch, iscratch);
+    launch_bi<double>(Lt, ldl, inv_t, scores, valid, used, L, thresh, s, scratch, iscratch, variant);
   else
-    launch_bi<float>(Lt, ldl, inv_t, scores, valid, used, L, thresh, s, scratch, iscratch);
+    launch_bi<float>(Lt, ldl, inv_t, scores, valid, used, L, thresh, s, scratch, iscratch, variant);
 }
 
 }  // namespace kern

@@ -29,7 +29,7 @@ void residual_partial(DType dt, int64_t M, int64_t N, int64_t K, const void* A, 
 // blockinv.hip
 void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                    int32_t* valid, const int32_t* used, const Layout& L, double thresh,
-                   hipStream_t s, void* scratch, int* iscratch);
+                   hipStream_t s, void* scratch, int* iscratch, int variant = -1);
 // blockinv_mfma.hip: 16 < m <= 128 (false = not handled)
 bool block_inverse_mfma(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                         int32_t* valid, const int32_t* used, const Layout& L, double thresh,
@@ -46,7 +46,8 @@ size_t block_inverse_big_scratch_bytes(DType dt, const Layout& L);
 bool block_inverse_co(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,
                       const int32_t* used, const Layout& L, double thresh, hipStream_t s, void* scratch);
 // scratch needed by the fp64 m > 128 paths (big kernel / generic sweep)
-size_t block_inverse_scratch_bytes(DType dt, const Layout& L);
+// (variant: the kernel family to use for this call, -1 = the process-wide setting)
+size_t block_inverse_scratch_bytes(DType dt, const Layout& L, int variant = -1);
 size_t block_inverse_iscratch_bytes(const Layout& L);
 
 // misc.hip

@@ -123,6 +123,21 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // the reservation at 100 GB/s, p = 2 / 4 are 9 / 6 % slower (profiles/cu_reserve_pgt1.md).
   if (rc < 0) rc = (dev_.on_gpu() && (L_.npad <= 16384 || small_rank)) ? 32 : 0;
   dev_.reserve_cus(rc, opt_.reserve_mode);
+  // Candidate inverses on ranks whose trailing update holds every CU (p > 1 without a reservation:
+  // the 16384- and 8192-row ranks of N = 32768) take the co-resident 4-wave form, which starts in
+  // the slot one retiring trailing-update workgroup frees instead of waiting for a whole CU: the
+  // p = 4 rank spends 616 of its 1154 us per step in a block inverse that alone takes ~100 us
+  // (profiles/rocprof_emu4_r2.md).  Rank-0 emulation at N = 32768, 100 GB/s model: p = 2 0.585 ->
+  // 0.576 s, p = 4 0.312 -> 0.299 s; on one GPU (and under the reservation) the register form stays
+  // (N = 32768: 1152.7 vs 1161.0 ms, profiles/blockinv_coresident.md).  GJ_BI_CORESIDENT=0/1
+  // overrides; an explicit process-wide GJ_BI_VARIANT wins.
+  {
+    const bool fits = opt_.dtype == DType::F64 && L_.m > 32 && L_.m <= 128;
+    bool co = dev_.on_gpu() && L_.p > 1 && rc == 0;
+    if (const char* e = std::getenv("GJ_BI_CORESIDENT")) co = std::atoi(e) != 0;
+    if (std::getenv("GJ_BI_VARIANT")) co = false;
+    bi_hint_ = (co && fits) ? 5 : -1;
+  }
 }
 
 Engine::~Engine() { free_buffers(); }
@@ -435,8 +450,11 @@ void Engine::select(int64_t t, const void* Lt) {
   const double thresh = opt_.eps * norm_a_;
   Range rg(opt_.profile, "gj:select");
   int pe = prof_begin(S_SIDE);
-  if (L_.nblk > 0)
+  if (L_.nblk > 0) {
+    dev_.set_block_inverse_hint(bi_hint_);  // per call: a device may be shared with other users
     dev_.block_inverse(opt_.dtype, Lt, L_.rows, inv_, scores_, valid_, used_, L_, thresh, S_SIDE);
+    dev_.set_block_inverse_hint(-1);
+  }
   if (L_.p == 1) {
     // one rank: the local record is the gathered set -> local argmin + book-keeping in one launch;
     // the result goes straight to pinned host memory (no copy kernel), the host polls its step field

@@ -191,16 +191,17 @@ def test_async_ranks_direct_bcast_on_one_gpu(p, monkeypatch):
     assert np.abs(asy - ref).max() / np.abs(ref).max() < 1e-8
 
 
-@pytest.mark.parametrize("bcast", ["ring", "direct"])
-def test_async_ranks_p8_driver_shape(bcast, monkeypatch):
-    """The engine configuration the 8-GPU scaling run gets (ranks of <= 4096 rows of an order above
-    16384: depth-8 panels, 32 reserved CUs, 8192-column chunks), on 8 stream-ordered virtual ranks
-    of one GPU with random arrival delays; both broadcast algorithms.  The residual must match the
+@pytest.mark.parametrize("p,bcast", [(8, "ring"), (8, "direct"), (2, "ring"), (3, "direct")])
+def test_async_ranks_driver_shapes(p, bcast, monkeypatch):
+    """The engine configurations the multi-GPU scaling run gets, on p stream-ordered virtual ranks of
+    one GPU with random arrival delays: p = 8 (ranks of <= 4096 rows of an order above 16384:
+    depth-8 panels, 32 reserved CUs, 8192-column chunks) and p = 2 / 3 (no reservation: the
+    co-resident candidate inverse), both broadcast algorithms.  The residual must match the
     single-GPU solve of the same matrix."""
     monkeypatch.setenv("GJ_BCAST", bcast)
     n, m = 16512, 128
     one = gj.GaussJordan(block_size=m, ranks=1, device="gpu").run(n, gen="random", seed=3)
-    rep = gj.GaussJordan(block_size=m, ranks=8, device="gpu", comm="async", jitter_us=50.0).run(
+    rep = gj.GaussJordan(block_size=m, ranks=p, device="gpu", comm="async", jitter_us=50.0).run(
         n, gen="random", seed=3)
     assert one["status"] == 0 and rep["status"] == 0, (one["message"], rep["message"])
     assert rep["residual"] < 10 * one["residual"] + 1e-9, (rep["residual"], one["residual"])
