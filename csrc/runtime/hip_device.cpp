@@ -233,12 +233,13 @@ void HipDevice::block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t
                               int s) {
   void* sc = nullptr;
   int* isc = nullptr;
-  const size_t b1 = kern::block_inverse_scratch_bytes(dt, L, bi_hint_);
+  const int variant = bi_hint_;  // one read: the scratch must match the kernel that is launched
+  const size_t b1 = kern::block_inverse_scratch_bytes(dt, L, variant);
   if (b1) {
     sc = scratch(b1, 0);
     isc = static_cast<int*>(scratch(kern::block_inverse_iscratch_bytes(L), 1));
   }
-  kern::block_inverse(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, hs(streams_[s]), sc, isc, bi_hint_);
+  kern::block_inverse(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, hs(streams_[s]), sc, isc, variant);
   check_launch();
 }
 void HipDevice::pivot_local(const double* scores, const int32_t* valid, const int32_t* used,
