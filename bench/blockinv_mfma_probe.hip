@@ -30,7 +30,7 @@ static void run(int m, int nblk) {
     (void)hipEventCreate(&e1);
     (void)hipEventRecord(e0, 0);
     hipLaunchKernelGGL((block_inverse_mfma_kernel<double, MP, RL>), dim3(nblk), dim3(64 * (NW + 1)), 0, 0, Lt,
-                       (int64_t)nblk * m, inv, scores, valid, used, m, (int64_t)1, (int64_t)0, 1e-12);
+                       (int64_t)nblk * m, inv, scores, valid, used, m, (int64_t)1, (int64_t)0, 1e-12, nullptr);
     (void)hipEventRecord(e1, 0);
     (void)hipDeviceSynchronize();
     float ms = 0;

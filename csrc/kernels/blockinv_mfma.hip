@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 #include <type_traits>
 #include <utility>
@@ -82,8 +83,15 @@ struct BiTile<float> {
 }  // namespace
 
 
-template <typename T, int MP, int PV>
-__global__ __launch_bounds__(64 * (MP / 16 + 1)) void block_inverse_mfma_kernel(
+// LAY = 1: the pivot wave gets a SIMD of its own.  The waves of a workgroup are placed on the four
+// SIMDs round-robin (hardware wave w -> SIMD w % 4), so hardware waves 4, 8, ... are left idle (they
+// only take part in the barriers): the pivot wave (hardware wave 0) then never shares its SIMD's
+// fp64 datapath with block-wave MFMAs.
+template <int MP, int LAY>
+constexpr int bim_hw_waves() { return MP / 16 + 1 + (LAY ? (MP / 16 - 1) / 3 : 0); }
+
+template <typename T, int MP, int PV, int LAY = 0>
+__global__ __launch_bounds__(64 * (MP / 16 + 1 + (LAY ? (MP / 16 - 1) / 3 : 0))) void block_inverse_mfma_kernel(
     const T* __restrict__ Lt, int64_t ldl, T* __restrict__ inv_t, double* __restrict__ scores,
     int32_t* __restrict__ valid, const int32_t* __restrict__ used, int m, int64_t p, int64_t k,
     double thresh, int32_t* __restrict__ piv_out) {
@@ -125,7 +133,28 @@ __global__ __launch_bounds__(64 * (MP / 16 + 1)) void block_inverse_mfma_kernel(
   __shared__ double redg[64 * NW / MP][MP];  // partial row abs-sums of the inverse
   __shared__ int s_sing;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hw = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+  int wave = hw;
+  if constexpr (LAY == 1) {
+    if (hw > 0 && (hw & 3) == 0) {
+      // idle wave: the pivot wave's barrier sequence, no work
+      __syncthreads();  // B0(0)
+      for (int q = 0; q < NP; ++q) {
+        __syncthreads();  // B1(q)
+        if (s_sing) break;
+        if (q + 1 < NP) __syncthreads();  // B0(q+1)
+      }
+      __syncthreads();  // E0
+      if (!s_sing)
+        for (int h = 0; h < 2; ++h) {
+          __syncthreads();  // E1(h)
+          __syncthreads();  // E2(h)
+        }
+      return;
+    }
+    wave = hw == 0 ? NW : hw - 1 - (hw >> 2);
+  }
+  const int tid = wave * 64 + lane;
   if (wave == 0) BIM_PROBE(1002);
   for (int i = tid; i < MP; i += NTH) kinv[i] = -1;
   if (tid == 0) s_sing = 0;
@@ -474,10 +503,21 @@ bool block_inverse_mfma(DType dt, const void* Lt, int64_t ldl, void* inv_t, doub
   if (grid == 0) return true;
   const int MP = m <= 32 ? 32 : m <= 64 ? 64 : 128;
   const dim3 blk(64 * (MP / 16 + 1));
-#define GJ_BI_LAUNCH1(T, MPV, PVV)                                                                \
-  hipLaunchKernelGGL((block_inverse_mfma_kernel<T, MPV, PVV>), dim3(grid), blk, 0, s,                \
-                     static_cast<const T*>(Lt), ldl, static_cast<T*>(inv_t), scores, valid, used, m, \
-                     L.p, L.k, thresh, g_piv_probe)
+  // pivot wave alone on its SIMD (LAY 1) where the block waves' MFMAs would share it (MP = 128: 8
+  // block waves): 96.0 -> 86.4 us per batch of 64 fp64 128 x 128 candidates (MP = 64: no change);
+  // GJ_BI_LAYOUT=0 restores the 9-wave layout
+  static const int lay = getenv("GJ_BI_LAYOUT") ? atoi(getenv("GJ_BI_LAYOUT")) : 1;
+#define GJ_BI_LAUNCH1(T, MPV, PVV)                                                                    \
+  do {                                                                                                \
+    if (lay == 1 && PVV == 2 && MPV == 128)                                                           \
+      hipLaunchKernelGGL((block_inverse_mfma_kernel<T, MPV, PVV, 1>), dim3(grid),                     \
+                         dim3(64 * bim_hw_waves<MPV, 1>()), 0, s, static_cast<const T*>(Lt), ldl,     \
+                         static_cast<T*>(inv_t), scores, valid, used, m, L.p, L.k, thresh, g_piv_probe); \
+    else                                                                                              \
+      hipLaunchKernelGGL((block_inverse_mfma_kernel<T, MPV, PVV>), dim3(grid), blk, 0, s,              \
+                         static_cast<const T*>(Lt), ldl, static_cast<T*>(inv_t), scores, valid, used, \
+                         m, L.p, L.k, thresh, g_piv_probe);                                           \
+  } while (0)
 #define GJ_BI_LAUNCH(T, MPV)   \
   if (pv == 2)                 \
     GJ_BI_LAUNCH1(T, MPV, 2);  \
