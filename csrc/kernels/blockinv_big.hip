@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 
 #include "kernels.hpp"
@@ -65,8 +66,10 @@ __device__ __forceinline__ double sum16(double v) {  // sum over the 16 lanes of
 // ~72 KiB of LDS, i.e. the footprint ONE retiring trailing-update workgroup frees on a CU (4 x 112
 // VGPRs per SIMD of GEMM + 64 spare; 4 x 26 KiB LDS + 56 spare), so a batch of candidate
 // inverses starts inside a running trailing update instead of waiting for whole CUs.
-template <int MP, int NB>
-__global__ __launch_bounds__(64 * (NB + 1)) void block_inverse_l2_kernel(
+// LAY = 1 (NB = 8): 11 hardware waves with 4 and 8 idle, so the pivot wave (hardware wave 0) has
+// SIMD 0 to itself (waves are placed on SIMDs round-robin), as in blockinv_mfma.hip.
+template <int MP, int NB, int LAY = 0>
+__global__ __launch_bounds__(64 * (NB + 1 + (LAY ? (NB - 1) / 3 : 0))) void block_inverse_l2_kernel(
     const double* __restrict__ Lt, int64_t ldl, double* __restrict__ inv_t, double* __restrict__ scores,
     int32_t* __restrict__ valid, const int32_t* __restrict__ used, int m, int64_t p, int64_t k,
     double thresh, double* __restrict__ scratch, int32_t* __restrict__ piv_out) {
@@ -95,7 +98,26 @@ __global__ __launch_bounds__(64 * (NB + 1)) void block_inverse_l2_kernel(
   __shared__ int kinv[MP];            // kinv[r] = column pivoted on row r
   __shared__ int s_sing;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hw = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+  int wave = hw;
+  if constexpr (LAY == 1) {
+    if (hw > 0 && (hw & 3) == 0) {
+      // idle wave: the pivot wave's barrier sequence, no work
+      __syncthreads();  // B0(0)
+      for (int q = 0; q < NT; ++q) {
+        __syncthreads();  // B1(q)
+        if (s_sing) break;
+        if (q + 1 < NT) __syncthreads();  // B0(q+1)
+      }
+      if (!s_sing) {
+        __syncthreads();  // E0
+        __syncthreads();  // E1
+      }
+      return;
+    }
+    wave = hw == 0 ? NB : hw - 1 - (hw >> 2);
+  }
+  const int tid = wave * 64 + lane;
   for (int i = tid; i < MP; i += 64 * (NB + 1)) kinv[i] = -1;
   if (tid == 0) s_sing = 0;
 
@@ -285,9 +307,15 @@ bool block_inverse_big(DType dt, const void* Lt, int64_t ldl, void* inv_t, doubl
   if (dt != DType::F64 || m <= 128 || m > 256) return false;
   const unsigned grid = (unsigned)L.nblk;
   if (grid == 0) return true;
-  hipLaunchKernelGGL((block_inverse_l2_kernel<256, 8>), dim3(grid), dim3(64 * 9), 0, s,
-                     static_cast<const double*>(Lt), ldl, static_cast<double*>(inv_t), scores, valid, used, m,
-                     L.p, L.k, thresh, static_cast<double*>(scratch), block_inverse_probe());
+  static const int lay = getenv("GJ_BI_LAYOUT") ? atoi(getenv("GJ_BI_LAYOUT")) : 1;
+  if (lay == 1)
+    hipLaunchKernelGGL((block_inverse_l2_kernel<256, 8, 1>), dim3(grid), dim3(64 * 11), 0, s,
+                       static_cast<const double*>(Lt), ldl, static_cast<double*>(inv_t), scores, valid, used, m,
+                       L.p, L.k, thresh, static_cast<double*>(scratch), block_inverse_probe());
+  else
+    hipLaunchKernelGGL((block_inverse_l2_kernel<256, 8>), dim3(grid), dim3(64 * 9), 0, s,
+                       static_cast<const double*>(Lt), ldl, static_cast<double*>(inv_t), scores, valid, used, m,
+                       L.p, L.k, thresh, static_cast<double*>(scratch), block_inverse_probe());
   return true;
 }
 
