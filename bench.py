@@ -8,8 +8,25 @@ native engine: look-ahead pivot search, chunk-pipelined RCCL pivot-row broadcast
 final row/column permutation into the reference's distribution.  GFLOP/s uses the nominal
 inversion count 2 N^3 and is the whole-job aggregate (strong scaling: N fixed).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]            # N = 1
-    torchrun --nproc-per-node N bench.py --gpus N --steps K ...    # N > 1 (one rank per GPU, RCCL)
+    python bench.py [--gpus N] [--steps K] [--warmup W]            # starts its own N rank processes
+    torchrun --nproc-per-node N bench.py --gpus N --steps K ...    # or one rank per process from torchrun
+
+Process model (the reference's SPMD start, main.cpp:65-74): one process per GPU.  Without
+torchrun's environment, ``--gpus N > 1`` makes this process a launcher that never touches a GPU: it
+starts N copies of itself with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, forwards rank 0's
+JSON line, stops the survivors when a rank fails, and exits with the largest child status.  The
+ranks bootstrap over gloo (the two RCCL unique ids, the timing barrier, the per-rank statistics);
+every collective of the solve is RCCL, issued by the native engine from C++.
+
+Failure handling: every host wait of the engine is bounded by ``--comm-timeout`` (default 90 s,
+below the driver's 600 s), so a hung peer turns into a non-zero exit on every rank, each naming
+its step, phase and the collective it sat in.
+
+``--same-gpu`` (rehearsal on a one-GPU box): all ranks share device 0 and RCCL is told that every
+rank is its own host (``NCCL_HOSTID``), so it accepts the duplicate device and connects the ranks
+through its network transport over loopback sockets.  This executes the multi-rank RCCL path
+(RcclComm's groups, broadcasts, all-gathers, point-to-point exchange) on one GPU; the timing is not
+an xGMI measurement.
 
 Rank 0 prints ONE JSON line.  vs_baseline divides by the reference's own measured rate (30.8 GFLOP/s
 nominal, its best published-in-survey run: N=8192, p=8 MPI ranks, SURVEY.md §7.5 — the reference
@@ -24,9 +41,10 @@ import sys
 import time
 
 REFERENCE_GFLOPS = 30.8  # reference N=8192 p=8 (35.73 s) -> 2N^3/t
+ROOT = os.path.dirname(os.path.abspath(__file__))
 
 
-def main() -> int:
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -38,8 +56,7 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--chunk-cols", type=int, default=0)
     ap.add_argument("--depth", type=int, default=0,
-                    help="elimination steps fused per trailing update (0 = the engine's choice: 2 up to "
-                         "N=8192, else 4, profiles/small_n_sweep.md)")
+                    help="elimination steps fused per trailing update (0 = the engine's choice)")
     ap.add_argument("--no-residual", action="store_true")
     ap.add_argument("--force-rccl", action="store_true", help="use the RCCL communicator even at 1 rank")
     ap.add_argument("--bcast", choices=["auto", "ring", "direct"], default=None,
@@ -50,64 +67,147 @@ def main() -> int:
                     help="cpu = the native host executor with gloo collectives (rehearses the exact "
                          "multi-rank script on a machine without GPUs; not a performance mode)")
     ap.add_argument("--host-threads", type=int, default=1, help="host executor threads per rank (--device cpu)")
-    args = ap.parse_args()
+    ap.add_argument("--comm-timeout", type=float, default=90.0,
+                    help="seconds a rank waits on a peer before it aborts the communicators and exits")
+    ap.add_argument("--profile", action="store_true",
+                    help="per-phase device timers; the JSON line carries the max over ranks")
+    ap.add_argument("--same-gpu", action="store_true",
+                    help="rehearsal: every rank on device 0, RCCL over loopback sockets (see above)")
+    return ap.parse_args(argv)
+
+
+# ----------------------------------------------------------------------------- launcher (no GPU)
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(args, argv) -> int:
+    """Start args.gpus rank processes of this script; never initialises a GPU itself."""
+    import subprocess
+    import threading
+
+    n = args.gpus
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *argv], env=env,
+                                      stdout=subprocess.PIPE, text=True, bufsize=1))
+
+    def forward(r, p):
+        for line in p.stdout:
+            if r == 0:
+                sys.stdout.write(line)
+                sys.stdout.flush()
+            else:
+                sys.stderr.write(f"[rank {r}] {line}")
+                sys.stderr.flush()
+
+    readers = [threading.Thread(target=forward, args=(r, p), daemon=True) for r, p in enumerate(procs)]
+    for t in readers:
+        t.start()
+    # A failed rank: its peers exit on their own once their communication timeout expires; give
+    # them that long (plus teardown), then stop whatever is left.
+    grace = args.comm_timeout + 30.0
+    deadline = None
+    while any(p.poll() is None for p in procs):
+        if deadline is None and any(p.returncode not in (None, 0) for p in procs):
+            deadline = time.monotonic() + grace
+        if deadline is not None and time.monotonic() > deadline:
+            for r, p in enumerate(procs):
+                if p.poll() is None:
+                    sys.stderr.write(f"bench.py: rank {r} still running {grace:.0f} s after a peer failed; killed\n")
+                    p.kill()
+            break
+        time.sleep(0.1)
+    codes = []
+    for p in procs:
+        rc = p.wait()
+        codes.append(rc if rc >= 0 else 128 - rc)
+    for t in readers:
+        t.join(timeout=5)
+    if any(codes):
+        sys.stderr.write(f"bench.py: rank exit codes {codes}\n")
+    return max(codes)
+
+
+# ----------------------------------------------------------------------------- one rank
+def run_rank(args) -> int:
     gpu = args.device == "gpu"
-
-    # Hardware queues and kernel-argument placement, before the first HIP call of the process
-    # (mpi_jordan_crazy_acceleration_amd/runtime_env.py: one queue per stream, so the two RCCL
-    # communicators' kernels never queue behind each other; device-memory kernel arguments).
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    from mpi_jordan_crazy_acceleration_amd.runtime_env import configure_runtime_env
-
-    configure_runtime_env()
-    if args.bcast:
-        os.environ["GJ_BCAST"] = args.bcast
-    import torch
-    import torch.distributed as dist
-
-    from mpi_jordan_crazy_acceleration_amd import load_native
-
-    C = load_native()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         return 2
+    if args.same_gpu:
+        local = 0
+        # RCCL refuses two ranks on one device of one host; as separate "hosts" they connect
+        # through the socket transport (loopback).  Read by RCCL at communicator creation.
+        os.environ["NCCL_HOSTID"] = f"gj-bench-rank{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
+
+    # Hardware queues and kernel-argument placement, before the first HIP call of the process
+    # (mpi_jordan_crazy_acceleration_amd/runtime_env.py).
+    sys.path.insert(0, ROOT)
+    from mpi_jordan_crazy_acceleration_amd.runtime_env import configure_runtime_env
+
+    configure_runtime_env()
+    if args.bcast:
+        os.environ["GJ_BCAST"] = args.bcast
+    from datetime import timedelta
+
+    import torch
+    import torch.distributed as dist
+
+    from mpi_jordan_crazy_acceleration_amd import load_native
+
+    C = load_native()
     if gpu:
         torch.cuda.set_device(local)
     if args.gemm_variant:
         C.set_gemm_variant(args.gemm_variant)
-    if not gpu:
-        dev = C.host_device(args.host_threads)
-        if world > 1:
-            from mpi_jordan_crazy_acceleration_amd.parallel.dist import TorchDistComm
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        # bootstrap only (ids, timing barrier, statistics); the solve's collectives are RCCL
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=timedelta(seconds=max(60.0, args.comm_timeout)))
 
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ.setdefault("MASTER_PORT", "29533")
-            dist.init_process_group("gloo", rank=rank, world_size=world)
-            comm = C.py_comm(TorchDistComm(), rank, world)
-        else:
-            comm = C.self_comm()
-    elif world > 1 or args.force_rccl:
-        if not dist.is_initialized():
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ.setdefault("MASTER_PORT", "29533")
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world)
-        ids = [[C.rccl_unique_id(), C.rccl_unique_id()] if rank == 0 else None]
-        dist.broadcast_object_list(ids, src=0)
-        dev = C.hip_device(local)
-        comm = C.rccl_comm(ids[0], world, rank, local)
-    else:
-        dev = C.hip_device(local)
-        comm = C.self_comm()
+    def fail(msg) -> int:
+        print(f"bench.py: rank {rank}: {msg}", file=sys.stderr, flush=True)
+        return 2
+
     try:
+        if not gpu:
+            dev = C.host_device(args.host_threads)
+            if world > 1:
+                from mpi_jordan_crazy_acceleration_amd.parallel.dist import TorchDistComm
+
+                comm = C.py_comm(TorchDistComm(), rank, world)
+            else:
+                comm = C.self_comm()
+        elif world > 1 or args.force_rccl:
+            ids = [[C.rccl_unique_id(), C.rccl_unique_id()] if rank == 0 else None]
+            if world > 1:
+                dist.broadcast_object_list(ids, src=0)
+            dev = C.hip_device(local)
+            comm = C.rccl_comm(ids[0], world, rank, local)
+        else:
+            dev = C.hip_device(local)
+            comm = C.self_comm()
         # allocation is agreed on every rank inside the constructor (a rank that cannot allocate
         # makes every rank fail here, before any other collective)
-        eng = C.Engine(dev, comm, args.n, args.m, args.dtype, args.chunk_cols, 1e-15, False, args.depth)
+        eng = C.Engine(dev, comm, args.n, args.m, args.dtype, args.chunk_cols, 1e-15, False, args.depth,
+                       args.profile, args.comm_timeout)
     except RuntimeError as e:
-        print(f"bench.py: rank {rank}: {e}", file=sys.stderr, flush=True)
-        return 2
+        return fail(e)
 
     def barrier():
         if dist.is_initialized():
@@ -119,36 +219,51 @@ def main() -> int:
         eng.generate(args.gen, args.seed)
         return eng.solve()
 
-    for _ in range(args.warmup):
-        st = step()
-        if st["status"] != 0:
-            print(f"bench.py: rank {rank}: solve failed with status {st['status']}", file=sys.stderr)
-            return 2
-    barrier()
-    t0 = time.perf_counter()
-    inner = []
-    for _ in range(args.steps):
-        st = step()
-        inner.append(st["seconds"])
-    barrier()
-    t1 = time.perf_counter()
+    try:
+        for _ in range(args.warmup):
+            st = step()
+            if st["status"] != 0:
+                return fail(f"solve failed with status {st['status']}")
+        barrier()
+        t0 = time.perf_counter()
+        stats = []
+        for _ in range(args.steps):
+            stats.append(step())
+        barrier()
+        t1 = time.perf_counter()
+    except RuntimeError as e:
+        return fail(e)
+    st = stats[-1] if stats else {"status": 0, "offdiag_pivots": 0, "host_wait_ms": 0.0, "seconds": 0.0}
     ms = (t1 - t0) * 1e3 / max(args.steps, 1)
+    mine = {
+        "ms": ms,
+        "solve_s": [s["seconds"] for s in stats],
+        "host_wait_ms": max([s["host_wait_ms"] for s in stats] or [0.0]),
+        "phases": stats[-1].get("phases") if stats else None,
+        "policy": eng.policy,
+    }
     if dist.is_initialized():
-        t = torch.tensor([ms, max(inner)], dtype=torch.float64, device="cuda" if gpu else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ms, inner_max = float(t[0]), float(t[1])
+        everyone = [None] * world
+        dist.all_gather_object(everyone, mine)
     else:
-        inner_max = max(inner)
+        everyone = [mine]
+    ms = max(e["ms"] for e in everyone)
     res = None
     if not args.no_residual and st["status"] == 0:
-        res = eng.residual_generated(args.gen, args.seed)
+        try:
+            res = eng.residual_generated(args.gen, args.seed)
+        except RuntimeError as e:
+            return fail(e)
     gflops = 2.0 * float(args.n) ** 3 / (ms / 1e3) / 1e9
     if rank == 0:
+        pol = dict(mine["policy"])
+        solve_all = [x for e in everyone for x in e["solve_s"]]
+        per_rank_max = [max(e["solve_s"] or [0.0]) for e in everyone]
         out = {
             "metric": "GFLOP/s + wall-clock, N=32768 dense Gauss-Jordan at 1/2/4/8 MI355X",
             "value": round(gflops, 3),
             "unit": "GFLOP/s (nominal 2N^3 per inversion, whole job)",
-            "n_gpus": world,
+            "n_gpus": 1 if args.same_gpu else world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 3),
@@ -163,24 +278,53 @@ def main() -> int:
                          "min-inverse-norm block pivoting)",
                 "global_batch": 1,
                 "seq_len": args.n,
-                "parallelism": (f"block-row-cyclic p={world} (" + ("RCCL over xGMI" if gpu else "gloo, host executor")
-                                + ")") if world > 1 else ("single GPU" if gpu else "single host rank"),
+                "parallelism": (f"block-row-cyclic p={world} (" +
+                                ("RCCL, ranks sharing one GPU over loopback sockets" if args.same_gpu else
+                                 "RCCL over xGMI" if gpu else "gloo, host executor") + ")")
+                               if world > 1 else ("single GPU" if gpu else "single host rank"),
                 "n": args.n,
                 "m": args.m,
-                "depth": eng.layout["depth"],
-                "bcast": eng.layout["bcast"],
+                "depth": pol["depth"],
+                "bcast": pol["bcast"],
             },
-            "bcast_tuning": comm.bcast_report(),
-            "solve_seconds_max": round(inner_max, 4),
+            "ranks": world,
+            "comm": pol.pop("comm"),
+            "bcast_tuning": pol.pop("bcast_tuning"),
+            "policy": pol,
+            "solve_seconds_max": round(max(solve_all or [0.0]), 4),
+            "solve_seconds_min": round(min(solve_all or [0.0]), 4),
+            "rank_solve_seconds_max": [round(x, 4) for x in per_rank_max],
+            "host_wait_ms_max": round(max(e["host_wait_ms"] for e in everyone), 3),
+            "host_wait_ms": round(st["host_wait_ms"], 3),
             "residual_inf": res,
             "status": st["status"],
             "offdiag_pivots": st["offdiag_pivots"],
-            "host_wait_ms": round(st["host_wait_ms"], 3),
         }
+        if args.same_gpu:
+            out["same_gpu_rehearsal"] = True
+        pols = [e["policy"] for e in everyone]
+        if any({k: v for k, v in p.items() if k != "comm"} != {k: v for k, v in pols[0].items() if k != "comm"}
+               for p in pols):
+            out["policy_per_rank"] = [{k: v for k, v in p.items() if k not in ("comm", "bcast_tuning")}
+                                      for p in pols]
+        if args.profile:
+            phases = {}
+            for e in everyone:
+                for name, v in (e["phases"] or {}).items():
+                    phases[name] = max(phases.get(name, 0.0), round(v["ms"], 3))
+            out["phases_ms_max"] = phases
         print(json.dumps(out), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
     return 0
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch(args, argv)
+    return run_rank(args)
 
 
 if __name__ == "__main__":

@@ -89,8 +89,17 @@ class Comm {
   void set_timeout(double seconds) { timeout_s_ = seconds; }
   double timeout() const { return timeout_s_; }
 
+  // Diagnostics: the last collective issued on each stream role (kind, root, bytes and its
+  // sequence number on that role).  Every timeout message names it, so a hang on a p-GPU node
+  // says which collective each rank sat in; ranks that disagree on the sequence number show
+  // which one fell behind.
+  void note(int s, const char* kind, size_t bytes, int root = -1);
+  std::string last_op(int s) const;
+
  protected:
   double timeout_s_ = 600;
+  std::string last_[kNumStreams];
+  uint64_t nops_[kNumStreams] = {};
   // Whether GJ_BCAST=auto measures (a GPU transport whose two algorithms differ in cost).
   virtual bool tunable() const { return false; }
   // Whether bcast_direct moves real data (false for the timing emulation, whose peers are synthetic).

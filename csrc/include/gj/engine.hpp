@@ -142,6 +142,16 @@ class Engine {
 
   int64_t real_local_rows() const;
   int depth() const { return d_; }  // elimination steps per panel (after the auto choice)
+  // What the auto policies chose on this rank (bench.py / --json report them).
+  struct Policy {
+    int depth = 0;
+    int64_t chunk_cols = 0;       // widest pivot-row chunk (columns)
+    int nchunks = 0;
+    int reserve_cus = 0;          // CUs kept off the trailing-update stream
+    std::string block_inverse;    // candidate-inverse kernel
+    bool comm_small_tiles = false;
+  };
+  Policy policy() const;
   const std::string& bcast_algo() const { return bcast_algo_; }  // "ring" | "direct"
 
  private:
@@ -159,6 +169,7 @@ class Engine {
   void chunk_pipeline(int64_t v, bool wait_main);
   void big_update(int64_t u);
   void finalize(const std::vector<int32_t>& seq);
+  SolveStats solve_steps();
   double residual_common(const void* A, bool wide);
   double residual_streamed(const void* A, bool wide);
   bool residual_wide();
@@ -197,6 +208,7 @@ class Engine {
   std::string bcast_algo_ = "ring";
   bool comm_small_tiles_ = false;  // COMM chunk-normalisation GEMMs on the small latency tile
   int bi_hint_ = -1;               // candidate-inverse kernel family (Device::set_block_inverse_hint)
+  int reserved_cus_ = 0;
   double norm_a_ = -1;
 
   // chunk plan (block-column ranges, multiples of d_ blocks so a panel never straddles chunks)
@@ -251,6 +263,10 @@ class Engine {
   bool block_mem_fail_ = false;
   bool last_residual_fp64_ = true;
   std::string block_mem_why_;
+  // where the solve is (named by communication-failure messages)
+  int64_t cur_step_ = -1;
+  const char* cur_phase_ = "setup";
+  int64_t hang_step_ = -1;  // GJ_TEST_HANG (fault injection)
 };
 
 }  // namespace gj

@@ -1075,6 +1075,19 @@ static void launch_bi(const void* Lt, int64_t ldl, void* inv_t, double* scores, 
                        valid, used, m, L.p, L.k, thresh, static_cast<T*>(scratch), iscratch);
 }
 
+// The kernel launch_bi picks (same decision tree), for the engine's policy report.
+const char* block_inverse_kernel_name(DType dt, int64_t m, int variant) {
+  const int v = variant >= 0 ? variant : bi_variant();
+  const bool f64 = dt == DType::F64;
+  if (v == 5 && f64 && m > 32 && m <= 128) return "l2_coresident";
+  if ((v == 0 || v == 3 || v == 4) && m > 16 && m <= 128) return "mfma_register";
+  if (v != 1 && f64 && m > 128 && m <= 256) return "l2_image";
+  if (v == 2 && m > 32 && m <= 128) return "panel_one_wave";
+  if (m <= 128 || (m <= 256 && !f64)) return "register_sweep";
+  if (v != 6 && m <= 1024) return "panel_blocked";
+  return "generic";
+}
+
 static bool generic_path(DType dt, int64_t m) { return dt == DType::F64 ? m > 128 : m > 256; }
 
 size_t block_inverse_scratch_bytes(DType dt, const Layout& L, int variant) {

@@ -22,6 +22,7 @@ int gemm_variant_id(const char* name);  // big | narrow | squarepf | bigpf | gld
 void set_gemm_variant(int v);
 void set_block_inverse_variant(int v);  // 0/3/4 = matrix-core panels (pipelined / LDS / readlane row bcast), 1 = sweep, 2 = one-wave panels
 int block_inverse_variant();
+const char* block_inverse_kernel_name(DType dt, int64_t m, int variant);
 void residual_partial(DType dt, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                       const void* B, int64_t ldb, int64_t n_real, int64_t blk_m, int64_t p,
                       int64_t k, double* partial, hipStream_t s);

@@ -49,44 +49,57 @@ class PyComm : public Comm {
   int size() const override { return n_; }
   int rank() const override { return r_; }
   std::string describe() const override { return "python(" + std::to_string(n_) + ")"; }
-  void allgather(Device& dev, const void* send, void* recv, size_t bytes, int) override {
+  void allgather(Device& dev, const void* send, void* recv, size_t bytes, int s) override {
     check(dev);
-    py::gil_scoped_acquire g;
-    impl_.attr("allgather")((uintptr_t)send, (uintptr_t)recv, bytes);
+    call(s, "allgather", bytes, -1, [&] { impl_.attr("allgather")((uintptr_t)send, (uintptr_t)recv, bytes); });
   }
-  void bcast(Device& dev, void* buf, size_t bytes, int root, int) override {
+  void bcast(Device& dev, void* buf, size_t bytes, int root, int s) override {
     check(dev);
-    py::gil_scoped_acquire g;
-    impl_.attr("bcast")((uintptr_t)buf, bytes, root);
+    call(s, "broadcast", bytes, root, [&] { impl_.attr("bcast")((uintptr_t)buf, bytes, root); });
   }
-  void allreduce_max(Device& dev, double* buf, size_t count, int) override {
+  void allreduce_max(Device& dev, double* buf, size_t count, int s) override {
     check(dev);
-    py::gil_scoped_acquire g;
-    impl_.attr("allreduce_max")((uintptr_t)buf, count);
+    call(s, "allreduce(max)", count * 8, -1, [&] { impl_.attr("allreduce_max")((uintptr_t)buf, count); });
   }
-  void group_p2p(Device& dev, const std::vector<P2POp>& ops, int) override {
+  void group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) override {
     check(dev);
-    py::gil_scoped_acquire g;
-    py::list l;
-    for (const auto& op : ops) l.append(py::make_tuple((uintptr_t)op.ptr, op.bytes, op.peer, op.send));
-    impl_.attr("group_p2p")(l);
+    size_t tot = 0;
+    for (const auto& op : ops) tot += op.bytes;
+    call(s, "grouped send/recv", tot, -1, [&] {
+      py::list l;
+      for (const auto& op : ops) l.append(py::make_tuple((uintptr_t)op.ptr, op.bytes, op.peer, op.send));
+      impl_.attr("group_p2p")(l);
+    });
   }
   void barrier(Device&) override {
-    py::gil_scoped_acquire g;
-    impl_.attr("barrier")();
+    call(S_SIDE, "barrier", 0, -1, [&] { impl_.attr("barrier")(); });
   }
   double host_max(Device&, double v) override {
-    py::gil_scoped_acquire g;
-    return impl_.attr("host_max")(v).cast<double>();
+    double out = 0;
+    call(S_SIDE, "host max", 8, -1, [&] { out = impl_.attr("host_max")(v).cast<double>(); });
+    return out;
   }
   void host_allgather(Device&, const void* send, void* recv, size_t bytes) override {
-    py::gil_scoped_acquire g;
-    impl_.attr("allgather")((uintptr_t)send, (uintptr_t)recv, bytes);
+    call(S_SIDE, "host allgather", bytes, -1,
+         [&] { impl_.attr("allgather")((uintptr_t)send, (uintptr_t)recv, bytes); });
   }
 
  private:
   static void check(Device& dev) {
     if (dev.on_gpu()) throw std::runtime_error("PyComm works on host memory only (use RcclComm on GPUs)");
+  }
+  // A Python-side failure (gloo timeout, a peer that closed its connection) becomes a
+  // communication error of the engine, converted while the GIL is held, naming the collective.
+  template <class F>
+  void call(int s, const char* kind, size_t bytes, int root, F&& f) {
+    note(s, kind, bytes, root);
+    py::gil_scoped_acquire g;
+    try {
+      f();
+    } catch (py::error_already_set& e) {
+      const std::string msg = e.what();
+      throw Error(Status::CommError, "torch.distributed failed in the " + last_op(s) + ": " + msg);
+    }
   }
   py::object impl_;
   int r_, n_;
@@ -390,6 +403,21 @@ PYBIND11_MODULE(_C, mod) {
                                d["rows"] = L.rows; d["real_rows"] = e.eng->real_local_rows();
                                d["depth"] = e.eng->depth();
                                d["bcast"] = e.eng->bcast_algo();
+                               return d;
+                             })
+      .def_property_readonly("policy",
+                             [](PyEngine& e) {
+                               const Engine::Policy pl = e.eng->policy();
+                               py::dict d;
+                               d["depth"] = pl.depth;
+                               d["chunk_cols"] = pl.chunk_cols;
+                               d["nchunks"] = pl.nchunks;
+                               d["reserve_cus"] = pl.reserve_cus;
+                               d["block_inverse"] = pl.block_inverse;
+                               d["comm_small_tiles"] = pl.comm_small_tiles;
+                               d["bcast"] = e.eng->bcast_algo();
+                               d["bcast_tuning"] = e.comm->bcast_report();
+                               d["comm"] = e.comm->describe();
                                return d;
                              })
       .def("generate",

@@ -73,6 +73,22 @@ void Comm::bcast_direct(Device& dev, const std::vector<BcastOp>& ops, int s) {
   group_p2p(dev, ph, s);
 }
 
+void Comm::note(int s, const char* kind, size_t bytes, int root) {
+  if (s < 0 || s >= kNumStreams) return;
+  char buf[160];
+  if (root >= 0)
+    std::snprintf(buf, sizeof buf, "#%llu %s root=%d bytes=%zu", (unsigned long long)++nops_[s], kind, root, bytes);
+  else
+    std::snprintf(buf, sizeof buf, "#%llu %s bytes=%zu", (unsigned long long)++nops_[s], kind, bytes);
+  last_[s] = buf;
+}
+
+std::string Comm::last_op(int s) const {
+  static const char* names[kNumStreams] = {"MAIN", "SIDE", "COMM", "MAIN2"};
+  if (s < 0 || s >= kNumStreams) return "?";
+  return std::string(names[s]) + " stream, last collective " + (last_[s].empty() ? "none" : last_[s]);
+}
+
 void Comm::drain(Device& dev, int s) {
   if (size() == 1 || !dev.on_gpu()) {
     dev.sync_stream(s);
@@ -90,8 +106,8 @@ void Comm::drain(Device& dev, int s) {
     if (std::chrono::duration<double>(t - t0).count() > timeout_s_) {
       abort();
       throw Error(Status::CommError, "timed out after " + std::to_string(timeout_s_) +
-                                         " s waiting for stream " + std::to_string(s) +
-                                         " behind a collective (peer failure or hang)");
+                                         " s waiting for the " + last_op(s) +
+                                         " (peer failure or hang)");
     }
     next = t + std::chrono::milliseconds(20);
   }

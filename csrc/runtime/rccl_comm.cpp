@@ -82,12 +82,14 @@ void* RcclComm::comm_for(int s) const {
 static inline hipStream_t st(Device& dev, int s) { return static_cast<hipStream_t>(dev.native_stream(s)); }
 
 void RcclComm::allgather(Device& dev, const void* send, void* recv, size_t bytes, int s) {
+  note(s, "ncclAllGather", bytes);
   NCCL_OK(ncclAllGather(send, recv, bytes, ncclUint8, static_cast<ncclComm_t>(comm_for(s)), st(dev, s)));
 }
 
 void RcclComm::bcast(Device& dev, void* buf, size_t bytes, int root, int s) {
   if (n_ == 1) return;
   if (use_direct(bytes)) return bcast_direct(dev, {BcastOp{buf, bytes, root}}, s);
+  note(s, "ncclBroadcast", bytes, root);
   NCCL_OK(ncclBroadcast(buf, buf, bytes, ncclUint8, root, static_cast<ncclComm_t>(comm_for(s)), st(dev, s)));
 }
 
@@ -95,6 +97,9 @@ void RcclComm::bcast_many(Device& dev, const std::vector<BcastOp>& ops, int s) {
   if (n_ == 1 || ops.empty()) return;
   ncclComm_t c = static_cast<ncclComm_t>(comm_for(s));
   std::vector<BcastOp> big;
+  size_t tot = 0;
+  for (const auto& o : ops) tot += o.bytes;
+  note(s, ops.size() == 1 ? "ncclBroadcast" : "grouped ncclBroadcast", tot, ops.front().root);
   NCCL_OK(ncclGroupStart());
   for (const auto& o : ops)
     if (use_direct(o.bytes)) big.push_back(o);
@@ -104,12 +109,16 @@ void RcclComm::bcast_many(Device& dev, const std::vector<BcastOp>& ops, int s) {
 }
 
 void RcclComm::allreduce_max(Device& dev, double* buf, size_t count, int s) {
+  note(s, "ncclAllReduce(max)", count * sizeof(double));
   NCCL_OK(ncclAllReduce(buf, buf, count, ncclFloat64, ncclMax, static_cast<ncclComm_t>(comm_for(s)), st(dev, s)));
 }
 
 void RcclComm::group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) {
   if (ops.empty()) return;
   ncclComm_t c = static_cast<ncclComm_t>(comm_for(s));
+  size_t tot = 0;
+  for (const auto& op : ops) tot += op.bytes;
+  note(s, "grouped ncclSend/ncclRecv", tot);
   NCCL_OK(ncclGroupStart());
   for (const auto& op : ops) {
     if (op.send)

@@ -22,6 +22,7 @@
 #include "gj/engine.hpp"
 
 #include "gj/io.hpp"
+#include "../kernels/kernels.hpp"
 
 #include <rocprofiler-sdk-roctx/roctx.h>
 
@@ -38,6 +39,43 @@ namespace {
 double now_s() {
   using clk = std::chrono::steady_clock;
   return std::chrono::duration<double>(clk::now().time_since_epoch()).count();
+}
+}  // namespace
+
+namespace {
+// `var`=<rank>:<tag>[,<rank>:<tag>...]: whether the list names (rank, tag).  Fault injection for
+// the failure-agreement tests:
+//   GJ_TEST_ALLOC_FAIL  tag = matrix | block | residual | residual_stream | residual64: that rank's
+//                       allocation of that stage fails;
+//   GJ_TEST_HANG        tag = a step number: that rank never issues the pivot exchange of that
+//                       step (a rank stuck in, or dead before, a collective).
+bool injected(const char* var, int rank, const std::string& tag) {
+  const char* e = std::getenv(var);
+  if (!e || !*e) return false;
+  const std::string all = e;
+  size_t b = 0;
+  while (b <= all.size()) {
+    const size_t end = std::min(all.find(',', b), all.size());
+    const std::string v = all.substr(b, end - b);
+    const size_t c = v.find(':');
+    if (c != std::string::npos && std::atoi(v.substr(0, c).c_str()) == rank && v.substr(c + 1) == tag) return true;
+    b = end + 1;
+  }
+  return false;
+}
+bool injected_alloc_fail(int rank, const char* stage) { return injected("GJ_TEST_ALLOC_FAIL", rank, stage); }
+int64_t injected_hang_step(int rank) {
+  const char* e = std::getenv("GJ_TEST_HANG");
+  if (!e || !*e) return -1;
+  const std::string all = e;
+  for (size_t b = 0; b <= all.size();) {
+    const size_t end = std::min(all.find(',', b), all.size());
+    const std::string v = all.substr(b, end - b);
+    const size_t c = v.find(':');
+    if (c != std::string::npos && std::atoi(v.substr(0, c).c_str()) == rank) return std::atoll(v.substr(c + 1).c_str());
+    b = end + 1;
+  }
+  return -1;
 }
 }  // namespace
 
@@ -72,6 +110,7 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
     for (int64_t b = cb0_[c]; b < cb1_[c]; ++b) chunk_of_[b] = (int64_t)c;
 
   comm_.set_timeout(opt_.comm_timeout_s);
+  hang_step_ = injected_hang_step(L_.k);
   // Allocation, agreed on every rank BEFORE any other collective (reference main.cpp:366-381 and
   // :428-436): 2 = this rank's matrix panels do not fit ("Not enough memory!", thrown on every
   // rank), 1 = the elimination work space does not ("not enough memory for block", reported by
@@ -122,7 +161,7 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // collectives need the free CUs: under the communication-cost model p = 8 is 6.6 % faster with
   // the reservation at 100 GB/s, p = 2 / 4 are 9 / 6 % slower (profiles/cu_reserve_pgt1.md).
   if (rc < 0) rc = (dev_.on_gpu() && (L_.npad <= 16384 || small_rank)) ? 32 : 0;
-  dev_.reserve_cus(rc, opt_.reserve_mode);
+  reserved_cus_ = dev_.reserve_cus(rc, opt_.reserve_mode);
   // Candidate inverses on ranks whose trailing update holds every CU (p > 1 without a reservation:
   // the 16384- and 8192-row ranks of N = 32768) take the co-resident 4-wave form, which starts in
   // the slot one retiring trailing-update workgroup frees instead of waiting for a whole CU: the
@@ -142,30 +181,23 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
 
 Engine::~Engine() { free_buffers(); }
 
+Engine::Policy Engine::policy() const {
+  Policy p;
+  p.depth = d_;
+  p.nchunks = (int)cb0_.size();
+  for (size_t c = 0; c < cb0_.size(); ++c) p.chunk_cols = std::max(p.chunk_cols, chunk_w((int64_t)c));
+  p.reserve_cus = reserved_cus_;
+  p.block_inverse = dev_.on_gpu() ? kern::block_inverse_kernel_name(opt_.dtype, L_.m, bi_hint_) : "host";
+  p.comm_small_tiles = comm_small_tiles_;
+  return p;
+}
+
 int64_t Engine::real_local_rows() const {
   if (L_.nblk == 0) return 0;
   const int64_t last_global_block = L_.global_block(L_.nblk - 1);
   return L_.rows - (last_global_block == L_.Nr - 1 ? (L_.m - L_.l_h) : 0);
 }
 
-namespace {
-// GJ_TEST_ALLOC_FAIL=<rank>:<stage>[,<rank>:<stage>...] makes that rank's allocation of that stage
-// (matrix | block | residual | residual_stream | residual64) fail (failure-agreement tests).
-bool injected_alloc_fail(int rank, const char* stage) {
-  const char* e = std::getenv("GJ_TEST_ALLOC_FAIL");
-  if (!e || !*e) return false;
-  const std::string all = e;
-  size_t b = 0;
-  while (b <= all.size()) {
-    const size_t end = std::min(all.find(',', b), all.size());
-    const std::string v = all.substr(b, end - b);
-    const size_t c = v.find(':');
-    if (c != std::string::npos && std::atoi(v.substr(0, c).c_str()) == rank && v.substr(c + 1) == stage) return true;
-    b = end + 1;
-  }
-  return false;
-}
-}  // namespace
 
 int Engine::alloc_buffers(std::string& why) {
   const int64_t m = L_.m, rows = std::max<int64_t>(L_.rows, 1), npad = L_.npad, dm = (int64_t)d_ * m;
@@ -321,7 +353,7 @@ void Engine::wait_pivot(int par, int64_t step, double& host_wait) {
         comm_.abort();
         throw Error(Status::CommError, "timed out after " + std::to_string(opt_.comm_timeout_s) +
                                            " s waiting for the pivot of step " + std::to_string(step) +
-                                           " (peer failure or hang)");
+                                           " behind the " + comm_.last_op(S_SIDE) + " (peer failure or hang)");
       }
       next_check = t + 0.02;
     }
@@ -465,6 +497,10 @@ void Engine::select(int64_t t, const void* Lt) {
   } else {
     dev_.pivot_local(scores_, valid_, used_, pos_, L_, myrec_, S_SIDE);
     prof_end(PH_PIVOT, pe, S_SIDE);
+    if (hang_step_ == t) {  // GJ_TEST_HANG: this rank never joins the exchange of step t
+      piv_host_[par].step = -1;
+      return;
+    }
     pe = prof_begin(S_SIDE);
     comm_.allgather(dev_, myrec_, recs_, sizeof(PivotRec), S_SIDE);
     piv_host_[par].step = -1;
@@ -495,6 +531,8 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
   const size_t es = esz();
   for (int64_t j = 0; j < q; ++j) {
     const int64_t t = t0 + j;
+    cur_step_ = t;
+    cur_phase_ = "pivot search";
     void* Lt = elem(At_[v % 3], j * m * rows);
     if (j == 0) {
       dev_.wait(S_SIDE, ev_L_);
@@ -522,6 +560,7 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
     }
     piv_[par][j] = r;
     st.pivots[t] = r.phys;
+    cur_phase_ = "panel piece";
     const bool owner = (r.owner == L_.k);
     const int64_t sl = r.phys / L_.p;
     int pe = prof_begin(S_SIDE);
@@ -600,6 +639,7 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
   const int64_t start = has_next ? chunk_of_[panel_t0(v + 1)] : 0;
   const int64_t pc0 = t0 * m, pc1 = (t0 + q) * m;  // panel columns
   dev_.wait(S_COMM, ev_pp_[par][q - 1]);  // all panel pieces, multiplier rows and H_t (SIDE)
+  cur_phase_ = "pivot-row broadcast";
   for (int64_t i = 0; i < C; ++i) {
     const int64_t c = (start + i) % C;
     const int64_t c0 = cb0_[c] * m, c1 = cb1_[c] * m, W = c1 - c0;
@@ -731,8 +771,23 @@ void Engine::big_update(int64_t u) {
 }
 
 // ---------------------------------------------------------------- solve
+// A communication failure names where this rank was: step, phase and the collective it sat in
+// (the message of the Comm / wait_pivot timeout), so a hang on a p-GPU node explains itself.
 SolveStats Engine::solve() {
+  try {
+    return solve_steps();
+  } catch (const Error& e) {
+    if (e.status() != Status::CommError) throw;
+    throw Error(Status::CommError, "rank " + std::to_string(L_.k) + "/" + std::to_string(L_.p) + ", step " +
+                                       std::to_string(cur_step_) + " of " + std::to_string(L_.Nr) +
+                                       ", phase " + cur_phase_ + ": " + e.what());
+  }
+}
+
+SolveStats Engine::solve_steps() {
   GJ_REQUIRE(!solved_, "solve(): input panel already consumed; load the matrix again");
+  cur_step_ = -1;
+  cur_phase_ = "norm";
   SolveStats st;
   const int64_t m = L_.m, Nr = L_.Nr, rows = L_.rows, npad = L_.npad;
   pmarks_.clear();
@@ -789,6 +844,7 @@ SolveStats Engine::solve() {
     dev_.wait(S_MAIN, ev_main2_);
   }
   {
+    cur_phase_ = "final exchange";
     const int pe = prof_begin(S_COMM);
     finalize(st.pivots);
     prof_end(PH_FINALIZE, pe, S_COMM);

@@ -86,3 +86,62 @@ def test_bench_alloc_failure_on_one_rank(stage, status):
             assert ("injected" if rank == 0 else "peer rank") in e
         else:
             assert f"status {status}" in e
+
+
+def _self_launch(nproc, *args, env_extra=None, timeout=240):
+    """`python bench.py --gpus N` with no torchrun environment: bench.py starts its own ranks."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra or {})
+    env.setdefault("OMP_NUM_THREADS", "1")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(nproc), "--device", "cpu", *args]
+    return subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_self_launch_matches_torchrun():
+    args = ("--steps", "2", "--warmup", "1", "--size", "200", "--block", "8", "--bcast", "direct")
+    a = _self_launch(8, *args)
+    assert a.returncode == 0, a.stderr[-3000:]
+    b = _torchrun(8, *args)
+    assert b.returncode == 0, b.stderr[-3000:]
+    da, db = _json_line(a.stdout), _json_line(b.stdout)
+    assert set(da) == set(db)
+    for k in ("n_gpus", "ranks", "steps", "warmup", "status", "offdiag_pivots", "config", "policy", "comm"):
+        assert da[k] == db[k], k
+    assert da["n_gpus"] == 8 and da["ranks"] == 8
+    assert da["residual_inf"] < 1e-8 and abs(da["residual_inf"] - db["residual_inf"]) < 1e-12
+    assert len(da["rank_solve_seconds_max"]) == 8
+    assert da["policy"]["depth"] == da["config"]["depth"]
+
+
+def test_bench_self_launch_failure_exit_code():
+    # one rank cannot allocate: the launcher's own exit status is the ranks' status 2
+    r = _self_launch(3, "--steps", "1", "--warmup", "1", "--size", "90", "--block", "8",
+                     env_extra={"GJ_TEST_ALLOC_FAIL": "1:matrix"})
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert "rank exit codes [2, 2, 2]" in r.stderr
+
+
+@pytest.mark.parametrize("launcher", ["self", "ranks"])
+def test_bench_hang_fails_fast(launcher):
+    """A rank that never joins the pivot exchange of step 3 (GJ_TEST_HANG): every rank exits
+    non-zero within the communication timeout and names the step (reference: none; a hung MPI
+    rank hangs the job)."""
+    import time
+    t0 = time.monotonic()
+    args = ("--steps", "1", "--warmup", "1", "--size", "200", "--block", "8", "--comm-timeout", "6")
+    env = {"GJ_TEST_HANG": "2:3"}
+    if launcher == "self":
+        r = _self_launch(4, *args, env_extra=env, timeout=120)
+        assert r.returncode == 2, r.stderr[-3000:]
+        errs = r.stderr
+        for rank in range(4):
+            assert f"bench.py: rank {rank}: rank {rank}/4, step 3 of 25" in errs, errs[-3000:]
+    else:
+        out = _ranks(4, *args, env_extra=env, timeout=120)
+        for rank, (rc, o, e) in enumerate(out):
+            assert rc == 2, (rank, rc, e[-2000:])
+            assert f"rank {rank}/4, step 3 of 25, phase pivot search" in e, e[-2000:]
+        assert "timed out after 6" in out[2][2]
+    assert time.monotonic() - t0 < 90
