@@ -33,15 +33,19 @@ def main():
                     help="cost-model bandwidths in GB/s (each also runs the comm-free baseline)")
     ap.add_argument("--lat", type=float, default=20.0, help="cost-model latency per collective, us")
     ap.add_argument("--channels", type=int, default=16, help="cost-model workgroups per collective")
+    ap.add_argument("--bcast", choices=["ring", "direct", "both"], default="ring",
+                    help="broadcast algorithm under the cost model (direct = scatter + slice exchange, "
+                         "two point-to-point rounds over p-1 links)")
     args = ap.parse_args()
     import torch  # noqa: F401  (shares libamdhip64 with the extension)
     from mpi_jordan_crazy_acceleration_amd import load_native
 
     C = load_native()
     dev = C.hip_device(0)
-    def run(p, d, bw):
-        comm = (C.shadow_comm(p, bw, args.lat if bw > 0 else 0.0, args.channels) if p > 1
-                else C.self_comm())
+    def run(p, d, bw, algo="ring"):
+        os.environ["GJ_BCAST"] = algo
+        comm = (C.shadow_comm(p, bw, args.lat if bw > 0 else 0.0, args.channels, direct=(algo == "direct"))
+                if p > 1 else C.self_comm())
         eng = C.Engine(dev, comm, args.size, args.block, args.dtype, args.chunk_cols, 1e-15, False, d)
         times, modelled = [], 0.0
         for _ in range(args.reps + 1):
@@ -69,10 +73,12 @@ def main():
                               "job_gflops_if_comm_free": round(2 * args.size ** 3 / t_free / 1e9, 1),
                               "rank_tflops": round(gemm_flops / t_free / 1e12, 2),
                               "host_wait_ms": round(st["host_wait_ms"], 1)}), flush=True)
-            for bw in (args.bw if p > 1 else []):
-                t, st, (rows, dd), modelled = run(p, d, bw)
+            algos = ["ring", "direct"] if args.bcast == "both" else [args.bcast]
+            for bw, algo in [(b, a) for b in (args.bw if p > 1 else []) for a in algos]:
+                t, st, (rows, dd), modelled = run(p, d, bw, algo)
                 hidden = 1.0 - (t - t_free) / modelled if modelled > 0 else None
-                print(json.dumps({"p": p, "depth": dd, "n": args.size, "model_bw_gbs": bw, "model_lat_us": args.lat,
+                print(json.dumps({"p": p, "depth": dd, "n": args.size, "bcast": algo if p > 2 else "ring",
+                                  "model_bw_gbs": bw, "model_lat_us": args.lat,
                                   "model_channels": args.channels, "status": st["status"],
                                   "seconds": round(t, 4),
                                   "job_gflops_cost_model": round(2 * args.size ** 3 / t / 1e9, 1),

@@ -100,15 +100,20 @@ class AsyncHostDevice : public Device {
   };
 
  private:
+  struct Op {
+    std::function<void()> f;
+    bool signal = false;
+  };
   struct Worker {
     std::thread th;
     std::mutex mu;
     std::condition_variable cv;
-    std::deque<std::function<void()>> q;
+    std::deque<Op> q;
     bool stop = false;
     std::mt19937_64 rng;
   };
-  void enqueue(int s, std::function<void()> f);
+  // signal = a fence / marker signal: still runs after a failure
+  void enqueue(int s, std::function<void()> f, bool signal = false);
   void run(int s);
   void fail(std::exception_ptr e);
   void rethrow();

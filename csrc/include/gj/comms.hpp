@@ -161,13 +161,18 @@ namespace gj {
 // stream for  lat_us + bytes / bandwidth  on `channels` workgroups of a spin kernel of RCCL's
 // footprint (256 threads, lds_kib of LDS), so a transfer both takes time on its stream AND
 // competes with the trailing-update GEMM for CUs, as RCCL's channel workgroups do.  Bandwidth is
-// the per-broadcast algorithm bandwidth (a ring broadcast delivers the whole message to every
-// rank at the rate of its slowest hop); the final block exchange runs over min(p-1, 7) links.
+// the per-link bandwidth: a ring broadcast delivers the whole message to every rank at the rate of
+// its slowest hop (one link); a group of point-to-point transfers (the direct broadcast's two
+// rounds, the final block exchange) takes as long as its busiest link.
 struct CostModel {
   double bw_gbs = 0;     // broadcast / point-to-point algorithm bandwidth, GB/s (0 = free comm)
   double lat_us = 0;     // per-collective latency (launch + handshake), us
   int channels = 16;     // workgroups a collective holds while it runs
   int lds_kib = 32;      // LDS per channel workgroup
+  // The direct broadcast (Comm::bcast_direct: root -> 1/(p-1) slices over p-1 links, then the
+  // slice exchange) is modelled as its two point-to-point rounds, each costing lat_us plus the
+  // busiest link's bytes / bw_gbs (every peer pair has its own xGMI link).  Off: ring only.
+  bool direct = false;
 };
 
 class ShadowComm : public Comm {
@@ -188,7 +193,7 @@ class ShadowComm : public Comm {
   double modelled_us() const { return modelled_us_; }  // total modelled transfer time issued
 
  protected:
-  bool direct_capable() const override { return false; }
+  bool direct_capable() const override { return cm_.direct; }
 
  private:
   void cost(Device& dev, size_t bytes, int links, int s);

@@ -138,6 +138,13 @@ class Device {
   // co-resident form, which the engine picks where its pivot chain waits for whole CUs).  Devices
   // with a single implementation ignore it.
   virtual void set_block_inverse_hint(int variant) { (void)variant; }
+  // Device scratch the candidate-inverse kernel family `variant` needs for layout L (bytes), and
+  // its allocation ahead of the first block_inverse call.
+  virtual size_t block_inverse_scratch_bytes(DType dt, const Layout& L, int variant) const {
+    (void)dt; (void)L; (void)variant;
+    return 0;
+  }
+  virtual void prepare_block_inverse(DType dt, const Layout& L, int variant) { (void)dt; (void)L; (void)variant; }
   // Local argmin over this rank's candidates -> *out.
   virtual void pivot_local(const double* scores, const int32_t* valid, const int32_t* used,
                            const int32_t* pos, const Layout& L, PivotRec* out, int s) = 0;

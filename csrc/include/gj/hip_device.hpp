@@ -58,6 +58,8 @@ class HipDevice : public Device {
                      int32_t* valid, const int32_t* used, const Layout& L, double thresh,
                      int s) override;
   void set_block_inverse_hint(int variant) override { bi_hint_ = variant; }
+  size_t block_inverse_scratch_bytes(DType dt, const Layout& L, int variant) const override;
+  void prepare_block_inverse(DType dt, const Layout& L, int variant) override;
   void pivot_local(const double* scores, const int32_t* valid, const int32_t* used,
                    const int32_t* pos, const Layout& L, PivotRec* out, int s) override;
   void pivot_select_single(const double* scores, const int32_t* valid, const Layout& L, int32_t t,

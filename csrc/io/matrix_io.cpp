@@ -67,6 +67,31 @@ int parse_token(const char* b, const char* e, double& v) {
   return q == e ? 1 : -1;
 }
 
+// Lexical test: the token is one plain decimal number ([sign] digits[.digits] [e[sign]digits]) that
+// strtod consumes completely.  Every other token (hex, inf/nan, glued numbers, garbage) is
+// "suspect" and gets the full parse_token, also in rows this rank does not keep: scanf's result for
+// the rows it keeps depends on every token before them (a glued "1.5-3" is two values, "zz" ends
+// the read), so every rank must see the same irregularities, not only the row's owner.
+inline bool plain_number(const char* b, const char* e) {
+  const char* s = b;
+  if (s < e && (*s == '+' || *s == '-')) ++s;
+  int digits = 0;
+  while (s < e && *s >= '0' && *s <= '9') ++s, ++digits;
+  if (s < e && *s == '.') {
+    ++s;
+    while (s < e && *s >= '0' && *s <= '9') ++s, ++digits;
+  }
+  if (digits == 0) return false;
+  if (s < e && (*s == 'e' || *s == 'E')) {
+    ++s;
+    if (s < e && (*s == '+' || *s == '-')) ++s;
+    int ed = 0;
+    while (s < e && *s >= '0' && *s <= '9') ++s, ++ed;
+    if (ed == 0) return false;
+  }
+  return s == e;
+}
+
 struct Mapping {
   const char* p = nullptr;
   size_t n = 0;
@@ -114,8 +139,9 @@ Status scan_sequential(const Mapping& mp, size_t need, int64_t ncols, const std:
 // ".bin", keeping the rows with rowpos[r] >= 0 at output row rowpos[r].  Text: the file is mapped;
 // pass 1 counts the tokens of every thread's chunk (chunks cut at whitespace), so every thread
 // knows the global index of its first token; pass 2 parses only the selected tokens straight into
-// the final buffer (no intermediate copies).  An irregular token (two numbers glued together)
-// makes the whole read fall back to the exact sequential scan.
+// the final buffer (no intermediate copies); the tokens of rows it does not keep get only the
+// lexical plain_number test.  An irregular token (two numbers glued together) anywhere among the
+// first nrows * ncols makes the whole read fall back to the exact sequential scan, on every rank.
 Status read_rows(const std::string& path, int64_t nrows, int64_t ncols, const std::vector<int64_t>& rowpos,
                  int64_t nsel, std::vector<double>& out, int nthreads) {
   const size_t need = (size_t)nrows * (size_t)ncols;
@@ -210,6 +236,18 @@ Status read_rows(const std::string& path, int64_t nrows, int64_t ncols, const st
           const char* t = p;
           while (t < e && !is_ws(*t)) ++t;
           const int64_t r = (int64_t)(idx / (size_t)ncols);
+          if (rowpos[r] < 0 && !plain_number(p, t)) {  // a row kept by another rank
+            double v;
+            const int ok = parse_token(p, t, v);
+            if (ok == 0) {
+              err[i] = 1;
+              return;
+            }
+            if (ok < 0 && idx + 1 < need) {
+              err[i] = 2;
+              return;
+            }
+          }
           if (rowpos[r] >= 0) {
             double v;
             const int ok = parse_token(p, t, v);

@@ -321,16 +321,17 @@ PYBIND11_MODULE(_C, mod) {
             py::gil_scoped_release rel;
             return std::shared_ptr<Comm>(new RcclComm(s, nranks, rank, device));
           });
-  mod.def("shadow_comm", [](int p, double bw_gbs, double lat_us, int channels, int lds_kib) {
+  mod.def("shadow_comm", [](int p, double bw_gbs, double lat_us, int channels, int lds_kib, bool direct) {
             CostModel cm;
             cm.bw_gbs = bw_gbs;
             cm.lat_us = lat_us;
             cm.channels = channels;
             cm.lds_kib = lds_kib;
+            cm.direct = direct;
             return std::shared_ptr<Comm>(new ShadowComm(p, cm));
           },
           py::arg("p"), py::arg("bw_gbs") = 0.0, py::arg("lat_us") = 0.0, py::arg("channels") = 16,
-          py::arg("lds_kib") = 32,
+          py::arg("lds_kib") = 32, py::arg("direct") = false,
           "rank 0 of a p-rank job alone on one device (critical-path timing emulation); bw_gbs > 0 "
           "adds the communication-cost model (lat_us + bytes/bw on `channels` spin workgroups)");
   mod.def("shadow_reset", [](std::shared_ptr<Comm> c) {

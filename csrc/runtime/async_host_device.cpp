@@ -59,20 +59,29 @@ void AsyncHostDevice::rethrow() {
   if (e) std::rethrow_exception(e);
 }
 
-// Worker loop: ops run in queue order; after the first failure the remaining ops are skipped
-// (markers and fences still signal, so no other stream hangs on a failed one).
+// Worker loop: ops run in queue order; after the first failure (any stream of this device) the
+// remaining ops are skipped, except markers and fences, which still signal so that no other stream
+// or host wait hangs on a failed one (a copy behind a timed-out wait_mark must not read a peer
+// buffer that is not ready).
 void AsyncHostDevice::run(int s) {
   Worker& w = w_[s];
   std::uniform_real_distribution<double> U(0.0, 1.0);
   for (;;) {
-    std::function<void()> f;
+    Op op;
     {
       std::unique_lock<std::mutex> lk(w.mu);
       w.cv.wait(lk, [&] { return w.stop || !w.q.empty(); });
       if (w.q.empty()) return;
-      f = std::move(w.q.front());
+      op = std::move(w.q.front());
       w.q.pop_front();
     }
+    bool failed;
+    {
+      std::lock_guard<std::mutex> lk(err_mu_);
+      failed = (bool)err_;
+    }
+    if (failed && !op.signal) continue;  // a failed device runs nothing but its signals
+    std::function<void()>& f = op.f;
     if (jitter_us_ > 0 && U(w.rng) < 0.25)
       std::this_thread::sleep_for(std::chrono::duration<double, std::micro>(U(w.rng) * jitter_us_));
     try {
@@ -83,12 +92,12 @@ void AsyncHostDevice::run(int s) {
   }
 }
 
-void AsyncHostDevice::enqueue(int s, std::function<void()> f) {
+void AsyncHostDevice::enqueue(int s, std::function<void()> f, bool signal) {
   check_stream(s);
   rethrow();
   Worker& w = w_[s];
   std::lock_guard<std::mutex> lk(w.mu);
-  w.q.push_back(std::move(f));
+  w.q.push_back(Op{std::move(f), signal});
   w.cv.notify_one();
 }
 
@@ -96,7 +105,7 @@ void AsyncHostDevice::enqueue(int s, std::function<void()> f) {
 void AsyncHostDevice::release(void* p) {
   for (int s = 0; s < kNumStreams; ++s) {
     auto f = std::make_shared<Fence>();
-    enqueue(s, [f] { f->signal(); });
+    enqueue(s, [f] { f->signal(); }, true);
     f->wait_for(1e9);
   }
   inner_.release(p);
@@ -104,7 +113,7 @@ void AsyncHostDevice::release(void* p) {
 void AsyncHostDevice::release_pinned(void* p) {
   for (int s = 0; s < kNumStreams; ++s) {
     auto f = std::make_shared<Fence>();
-    enqueue(s, [f] { f->signal(); });
+    enqueue(s, [f] { f->signal(); }, true);
     f->wait_for(1e9);
   }
   inner_.release_pinned(p);
@@ -137,7 +146,7 @@ void AsyncHostDevice::record(int ev, int s) {
     std::lock_guard<std::mutex> lk(ev_mu_);
     ev_last_.at(ev) = f;
   }
-  enqueue(s, [f] { f->signal(); });
+  enqueue(s, [f] { f->signal(); }, true);
 }
 // Like hipStreamWaitEvent: waits for the record issued last before this call (none: no wait).
 void AsyncHostDevice::wait(int s, int ev) {
@@ -169,7 +178,7 @@ bool AsyncHostDevice::query_event(int ev) {
 }
 void AsyncHostDevice::sync_stream(int s) {
   auto f = std::make_shared<Fence>();
-  enqueue(s, [f] { f->signal(); });
+  enqueue(s, [f] { f->signal(); }, true);
   if (!f->wait_for(wait_timeout_s_ * 4)) throw Error(Status::CommError, "host-async: stream synchronisation timed out");
   rethrow();
 }
@@ -190,7 +199,7 @@ float AsyncHostDevice::event_ms(int a, int b) {
 }
 std::shared_ptr<void> AsyncHostDevice::mark(int s) {
   auto f = std::make_shared<Fence>();
-  enqueue(s, [f] { f->signal(); });
+  enqueue(s, [f] { f->signal(); }, true);
   return f;
 }
 void AsyncHostDevice::wait_mark(int s, const std::shared_ptr<void>& h) {

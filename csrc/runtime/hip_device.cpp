@@ -228,6 +228,16 @@ void HipDevice::add_diag(DType dt, void* A, int64_t ld, int64_t nd, double alpha
   kern::add_diag(dt, A, ld, nd, alpha, hs(streams_[s]));
   check_launch();
 }
+size_t HipDevice::block_inverse_scratch_bytes(DType dt, const Layout& L, int variant) const {
+  const size_t b1 = kern::block_inverse_scratch_bytes(dt, L, variant);
+  return b1 ? b1 + kern::block_inverse_iscratch_bytes(L) : 0;
+}
+void HipDevice::prepare_block_inverse(DType dt, const Layout& L, int variant) {
+  const size_t b1 = kern::block_inverse_scratch_bytes(dt, L, variant);
+  if (!b1) return;
+  scratch(b1, 0);
+  scratch(kern::block_inverse_iscratch_bytes(L), 1);
+}
 void HipDevice::block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                               int32_t* valid, const int32_t* used, const Layout& L, double thresh,
                               int s) {

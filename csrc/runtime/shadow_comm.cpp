@@ -10,8 +10,8 @@ namespace gj {
 std::string ShadowComm::describe() const {
   std::string d = "shadow(" + std::to_string(p_);
   if (cm_.bw_gbs > 0)
-    d += ", cost model " + std::to_string(cm_.bw_gbs) + " GB/s + " + std::to_string(cm_.lat_us) + " us on " +
-         std::to_string(cm_.channels) + " workgroups";
+    d += ", cost model " + std::to_string(cm_.bw_gbs) + " GB/s per link + " + std::to_string(cm_.lat_us) +
+         " us on " + std::to_string(cm_.channels) + " workgroups" + (cm_.direct ? ", direct broadcast" : "");
   return d + ")";
 }
 
@@ -23,9 +23,13 @@ void ShadowComm::cost(Device& dev, size_t bytes, int links, int s) {
 }
 
 void ShadowComm::group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) {
-  size_t out = 0, in = 0;  // the busier direction bounds the exchange
-  for (const auto& o : ops) (o.send ? out : in) += o.bytes;
-  if (!ops.empty()) cost(dev, std::max(out, in), std::min(p_ - 1, 7), s);
+  // one link per peer and direction (fully connected xGMI): the busiest link bounds the group
+  if (ops.empty()) return;
+  std::vector<size_t> out((size_t)p_, 0), in((size_t)p_, 0);
+  for (const auto& o : ops) (o.send ? out : in)[(size_t)o.peer] += o.bytes;
+  size_t busiest = 0;
+  for (int q = 0; q < p_; ++q) busiest = std::max({busiest, out[q], in[q]});
+  cost(dev, busiest, 1, s);
 }
 
 void ShadowComm::allgather(Device& dev, const void* send, void* recv, size_t bytes, int s) {
@@ -51,6 +55,7 @@ void ShadowComm::allgather(Device& dev, const void* send, void* recv, size_t byt
 }
 
 void ShadowComm::bcast(Device& dev, void* buf, size_t bytes, int root, int s) {
+  if (use_direct(bytes)) return bcast_direct(dev, {BcastOp{buf, bytes, root}}, s);
   cost(dev, bytes, 1, s);
   if (root != 0) dev.memset0(buf, bytes, s);
 }

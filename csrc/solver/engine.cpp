@@ -109,6 +109,35 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   for (size_t c = 0; c < cb0_.size(); ++c)
     for (int64_t b = cb0_[c]; b < cb1_[c]; ++b) chunk_of_[b] = (int64_t)c;
 
+  // CU reservation for the latency-bound panel factorisation (GJ_RESERVE_CUS overrides).
+  int rc = opt_.reserve_cus;
+  if (const char* e = std::getenv("GJ_RESERVE_CUS")) rc = std::atoi(e);
+  if (const char* e = std::getenv("GJ_RESERVE_MODE")) opt_.reserve_mode = std::atoi(e);
+  // auto: up to N = 16384 the pivot chain is the critical path and its block inverses only start
+  // on a CU no trailing-update workgroup occupies, so keep 32 CUs (1/8 of the chip) off the MAIN
+  // streams: N=8192 p=1 -12 %, emulated p=2/4/8 at N=16384 -10/-16/-14 %.  At N=32768 the GEMM is
+  // the critical path and the mask costs 4-10 % (profiles/cu_reserve_sweep.md) -- except on ranks
+  // with <= 4096 rows (p = 8 at N = 32768), where the pivot chain and the RCCL workgroups of its
+  // collectives need the free CUs: under the communication-cost model p = 8 is 6.6 % faster with
+  // the reservation at 100 GB/s, p = 2 / 4 are 9 / 6 % slower (profiles/cu_reserve_pgt1.md).
+  if (rc < 0) rc = (dev_.on_gpu() && (L_.npad <= 16384 || small_rank)) ? 32 : 0;
+  reserved_cus_ = dev_.reserve_cus(rc, opt_.reserve_mode);
+  // Candidate inverses on ranks whose trailing update holds every CU (p > 1 without a reservation:
+  // the 16384- and 8192-row ranks of N = 32768) take the co-resident 4-wave form, which starts in
+  // the slot one retiring trailing-update workgroup frees instead of waiting for a whole CU: the
+  // p = 4 rank spends 616 of its 1154 us per step in a block inverse that alone takes ~100 us
+  // (profiles/rocprof_emu4_r2.md).  Rank-0 emulation at N = 32768, 100 GB/s model: p = 2 0.585 ->
+  // 0.576 s, p = 4 0.312 -> 0.299 s; on one GPU (and under the reservation) the register form stays
+  // (N = 32768: 1152.7 vs 1161.0 ms, profiles/blockinv_coresident.md).  GJ_BI_CORESIDENT=0/1
+  // overrides; an explicit process-wide GJ_BI_VARIANT wins.
+  {
+    const bool fits = opt_.dtype == DType::F64 && L_.m > 32 && L_.m <= 128;
+    bool co = dev_.on_gpu() && L_.p > 1 && rc == 0;
+    if (const char* e = std::getenv("GJ_BI_CORESIDENT")) co = std::atoi(e) != 0;
+    if (std::getenv("GJ_BI_VARIANT")) co = false;
+    bi_hint_ = (co && fits) ? 5 : -1;
+  }
+
   comm_.set_timeout(opt_.comm_timeout_s);
   hang_step_ = injected_hang_step(L_.k);
   // Allocation, agreed on every rank BEFORE any other collective (reference main.cpp:366-381 and
@@ -149,34 +178,6 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   if (const char* e = std::getenv("GJ_COMM_SMALL_TILES")) comm_small_tiles_ = std::atoi(e) != 0;
   two_main_ = two_main_ && cb0_.size() > 1;
 
-  // CU reservation for the latency-bound panel factorisation (GJ_RESERVE_CUS overrides).
-  int rc = opt_.reserve_cus;
-  if (const char* e = std::getenv("GJ_RESERVE_CUS")) rc = std::atoi(e);
-  if (const char* e = std::getenv("GJ_RESERVE_MODE")) opt_.reserve_mode = std::atoi(e);
-  // auto: up to N = 16384 the pivot chain is the critical path and its block inverses only start
-  // on a CU no trailing-update workgroup occupies, so keep 32 CUs (1/8 of the chip) off the MAIN
-  // streams: N=8192 p=1 -12 %, emulated p=2/4/8 at N=16384 -10/-16/-14 %.  At N=32768 the GEMM is
-  // the critical path and the mask costs 4-10 % (profiles/cu_reserve_sweep.md) -- except on ranks
-  // with <= 4096 rows (p = 8 at N = 32768), where the pivot chain and the RCCL workgroups of its
-  // collectives need the free CUs: under the communication-cost model p = 8 is 6.6 % faster with
-  // the reservation at 100 GB/s, p = 2 / 4 are 9 / 6 % slower (profiles/cu_reserve_pgt1.md).
-  if (rc < 0) rc = (dev_.on_gpu() && (L_.npad <= 16384 || small_rank)) ? 32 : 0;
-  reserved_cus_ = dev_.reserve_cus(rc, opt_.reserve_mode);
-  // Candidate inverses on ranks whose trailing update holds every CU (p > 1 without a reservation:
-  // the 16384- and 8192-row ranks of N = 32768) take the co-resident 4-wave form, which starts in
-  // the slot one retiring trailing-update workgroup frees instead of waiting for a whole CU: the
-  // p = 4 rank spends 616 of its 1154 us per step in a block inverse that alone takes ~100 us
-  // (profiles/rocprof_emu4_r2.md).  Rank-0 emulation at N = 32768, 100 GB/s model: p = 2 0.585 ->
-  // 0.576 s, p = 4 0.312 -> 0.299 s; on one GPU (and under the reservation) the register form stays
-  // (N = 32768: 1152.7 vs 1161.0 ms, profiles/blockinv_coresident.md).  GJ_BI_CORESIDENT=0/1
-  // overrides; an explicit process-wide GJ_BI_VARIANT wins.
-  {
-    const bool fits = opt_.dtype == DType::F64 && L_.m > 32 && L_.m <= 128;
-    bool co = dev_.on_gpu() && L_.p > 1 && rc == 0;
-    if (const char* e = std::getenv("GJ_BI_CORESIDENT")) co = std::atoi(e) != 0;
-    if (std::getenv("GJ_BI_VARIANT")) co = false;
-    bi_hint_ = (co && fits) ? 5 : -1;
-  }
 }
 
 Engine::~Engine() { free_buffers(); }
@@ -207,7 +208,8 @@ int Engine::alloc_buffers(std::string& why) {
   for (size_t c = 0; c < cb0_.size(); ++c) wmax = std::max(wmax, chunk_w((int64_t)c));
   const size_t need_matrix = 2 * panel;
   const size_t need_work = 3 * (size_t)dm * rows * es + 2 * (size_t)dm * npad * es +
-                           (size_t)std::max<int64_t>(L_.nblk, 1) * m * m * es + (size_t)m * wmax * es;
+                           (size_t)std::max<int64_t>(L_.nblk, 1) * m * m * es + (size_t)m * wmax * es +
+                           dev_.block_inverse_scratch_bytes(opt_.dtype, L_, bi_hint_);
   const size_t avail = dev_.on_gpu() ? dev_.free_memory() : SIZE_MAX;
   auto fits = [&](size_t need) { return !dev_.on_gpu() || need + (64u << 20) <= avail; };
   // stage 1: the matrix panels (the reference's a / b arrays)
@@ -256,6 +258,8 @@ void Engine::alloc_work(int64_t wmax) {
   T_ = dev_.alloc((size_t)m * wmax * es);
   RP_ = dev_.alloc((size_t)m * dm * es);
   inv_ = dev_.alloc((size_t)std::max<int64_t>(L_.nblk, 1) * m * m * es);
+  // the candidate-inverse kernel's scratch, now: not lazily inside the first timed pivot search
+  dev_.prepare_block_inverse(opt_.dtype, L_, bi_hint_);
   scores_ = static_cast<double*>(dev_.alloc(sizeof(double) * std::max<int64_t>(L_.nblk, 1)));
   valid_ = static_cast<int32_t*>(dev_.alloc(sizeof(int32_t) * std::max<int64_t>(L_.nblk, 1)));
   pos_ = static_cast<int32_t*>(dev_.alloc(sizeof(int32_t) * L_.Nr));
@@ -443,9 +447,11 @@ Status Engine::read_file_rows(const std::string& path, int nthreads, std::vector
   mine.reserve((size_t)real);
   for (int64_t r = 0; r < real; ++r) mine.push_back(L_.global_row(r));
   Status s = Status::Ok;
+  if (nthreads <= 0)  // the p ranks of a node share its cores
+    nthreads = (int)std::max<int64_t>(1, (int64_t)std::max(1u, std::thread::hardware_concurrency()) / L_.p);
   try {
     s = read_matrix_rows(path, L_.n, mine, rows, nthreads);
-  } catch (const std::bad_alloc&) {
+  } catch (const std::exception&) {  // bad_alloc, thread creation (system_error), ...: agreed below
     s = Status::CannotRead;
   }
   if (comm_.host_max(dev_, s == Status::CannotOpen ? 1.0 : 0.0) > 0) return Status::CannotOpen;
@@ -1241,6 +1247,11 @@ RhsResult Engine::solve_rhs(const double* b, double* x, const GenSpec* gen, cons
     const double an = comm_.host_max(dev_, L_.nblk > 0 ? dhost_[0] : 0.0);
     apply_inverse(b, x);
     std::vector<double> r((size_t)n), d((size_t)n);
+    // the best iterate so far (a diverging refinement, e.g. an fp32 inverse with ||I - XA|| near 1,
+    // must not hand back a worse x than it was given)
+    std::vector<double> best_x(x, x + n);
+    RhsResult best;
+    double best_rn = 1e300;
     double prev = 1e300;
     for (int it = 0;; ++it) {
       // r = b - A x (this rank's rows, fp64), all-gathered to the full vector
@@ -1273,8 +1284,19 @@ RhsResult Engine::solve_rhs(const double* b, double* x, const GenSpec* gen, cons
         rr.converged = true;
         break;
       }
-      if (it >= max_refine) break;
-      if (it > 0 && rn > 0.5 * prev) break;  // not contracting: refinement cannot converge here
+      if (rn < best_rn) {
+        best_rn = rn;
+        best_x.assign(x, x + n);
+        best = rr;
+      }
+      if (it >= max_refine || (it > 0 && rn > 0.5 * prev)) {  // budget spent / not contracting
+        if (rn > best_rn) {  // return the best iterate, with its own residual (history kept)
+          std::copy(best_x.begin(), best_x.end(), x);
+          best.history = rr.history;
+          rr = best;
+        }
+        break;
+      }
       prev = rn;
       apply_inverse(r.data(), d.data());
       for (int64_t i = 0; i < n; ++i) x[i] += d[(size_t)i];

@@ -66,12 +66,34 @@ def test_reader_bad_token_late_chunk(native, tmp_path, where):
     f.write_text(" ".join(toks_bad))
     with pytest.raises(RuntimeError, match="cannot read"):
         native.read_matrix_file(str(f), n)
+    # scanf stops at "zz" whichever rank keeps its row: every rank reports the failure
     r_bad = bad // n
     other = [r for r in range(n) if r != r_bad][:50]
-    assert np.array_equal(native.read_matrix_rows(str(f), n, other), A[other])
+    with pytest.raises(RuntimeError, match="cannot read"):
+        native.read_matrix_rows(str(f), n, other)
     # irregular: tokens i and i+1 glued as "a-b" (b negative) -> same numbers, sequential scan
     i = next(j for j in range(bad // 2, len(toks) - 1) if toks[j + 1].startswith("-"))
     toks_irr = toks[:i] + [toks[i] + toks[i + 1]] + toks[i + 2:]
     g = tmp_path / "irr.txt"
     g.write_text(" ".join(toks_irr))
     assert np.array_equal(native.read_matrix_file(str(g), n), A)
+
+
+@pytest.mark.parametrize("nt", [1, 4])
+def test_reader_glued_token_outside_requested_rows(native, tmp_path, nt):
+    # a glued "a-b" in a row another rank keeps shifts every later value under scanf;
+    # a rank reading only OTHER rows must see the shift too (sequential fallback on every rank)
+    n = 400
+    A = np.random.default_rng(4).standard_normal((n, n))
+    toks = [f"{v:.17g}" for v in A.ravel()]
+    i = next(j for j in range(n * 10, len(toks) - 1) if toks[j + 1].startswith("-"))
+    glued_row = i // n
+    toks_irr = toks[:i] + [toks[i] + toks[i + 1]] + toks[i + 2:] + ["0.5"]
+    g = tmp_path / "irr_other.txt"
+    g.write_text(" ".join(toks_irr))
+    later = [r for r in range(glued_row + 1, n, 7)]
+    earlier = [r for r in range(0, glued_row, 3)]
+    rows = earlier + later
+    assert glued_row not in rows
+    got = native.read_matrix_rows(str(g), n, rows, nt)
+    assert np.array_equal(got, A[rows])

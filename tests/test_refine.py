@@ -60,3 +60,15 @@ def test_gpu_fp32_refinement(n, m):
     assert r["status"] == 0 and r["residual_fp64"] is True
     assert r["refine_converged"], r["axb_history"]
     assert r["axb_history"][-1] < 1e-10
+
+
+@pytest.mark.parametrize("n,m", [(12, 3), (16, 4)])
+def test_diverging_refinement_returns_best_iterate(n, m):
+    # an fp32 inverse of a Hilbert matrix (kappa ~ 1e16) makes refinement diverge; the
+    # returned x and its residual must be the best iterate's, not the last one's
+    r = GaussJordan(block_size=m, device="cpu", dtype="fp32").run(n, gen="hilbert", rhs="ones")
+    assert r["status"] == 0 and not r["refine_converged"]
+    h = r["axb_history"]
+    assert len(h) >= 2 and h[-1] > h[0]
+    assert r["axb_residual"] == pytest.approx(min(h), rel=1e-12)  # ||b||_inf = 1
+    assert r["refine_steps"] == h.index(min(h))
