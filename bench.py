@@ -181,8 +181,11 @@ def run_rank(args) -> int:
                                 timeout=timedelta(seconds=max(60.0, args.comm_timeout)))
 
     def fail(msg) -> int:
+        # a failed rank leaves at once: its communicators may be aborted or hung on a dead peer,
+        # and their teardown (or the bootstrap group's) must not decide the exit status
         print(f"bench.py: rank {rank}: {msg}", file=sys.stderr, flush=True)
-        return 2
+        sys.stdout.flush()
+        os._exit(2)
 
     try:
         if not gpu:
