@@ -1,6 +1,12 @@
-"""The one-process-per-GPU deployment path on the MI355X: bench.py under torch.distributed.run with
-the RCCL communicator (world size 1 on a one-GPU box: RCCL communicator creation, all-gather of
-pivot records, RCCL all-reduce of the timing/residual maxima; broadcasts are rank-local)."""
+"""The one-process-per-GPU deployment path on the MI355X: bench.py with the RCCL communicator.
+
+* world size 1 under torch.distributed.run (RCCL communicator creation, all-gather of pivot
+  records, all-reduce of the timing/residual maxima; broadcasts are rank-local);
+* world size 2 / 3 on the one GPU (`--same-gpu`: every rank its own RCCL "host", connected by
+  RCCL's socket transport): the engine's real RCCL schedule at p > 1 — grouped ncclBroadcast of
+  pivot-row chunks (ring, or the direct scatter + exchange over ncclSend/ncclRecv), ncclAllGather
+  of pivot records, the grouped point-to-point final exchange — must give the p = 1 inverse.
+  (profiles/rccl_same_gpu_r3.md)"""
 import json
 import os
 import subprocess
@@ -34,3 +40,25 @@ def test_cli_with_rccl_communicator():
     assert "glob_time:" in out.stdout and "residual:" in out.stdout
     rep = json.loads([l for l in out.stderr.splitlines() if l.startswith("{")][-1])
     assert rep["status"] == 0 and rep["comm"].startswith("rccl") and rep["residual"] < 1e-6
+
+
+def _self_launch(*args, timeout=300):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], cwd=ROOT, env=env,
+                         capture_output=True, text=True, timeout=timeout)
+    assert out.returncode == 0, out.stderr[-3000:]
+    return json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+
+
+@pytest.mark.parametrize("ranks,bcast", [(2, "ring"), (3, "direct")])
+def test_rccl_multi_rank_same_gpu(ranks, bcast):
+    common = ("--steps", "1", "--warmup", "1", "--size", "2048", "--block", "128", "--comm-timeout", "60")
+    one = _self_launch("--gpus", "1", "--force-rccl", *common)
+    rep = _self_launch("--gpus", str(ranks), "--same-gpu", "--bcast", bcast, *common)
+    assert rep["status"] == 0 and rep["ranks"] == ranks
+    assert rep["comm"].startswith("rccl(") and rep["comm"].endswith(f"{ranks} ranks)")
+    assert rep["config"]["bcast"] == ("direct" if ranks > 2 and bcast == "direct" else "ring")
+    assert rep["residual_inf"] < 1e-8
+    assert abs(rep["residual_inf"] - one["residual_inf"]) <= 1e-3 * one["residual_inf"]
+    assert len(rep["rank_solve_seconds_max"]) == ranks
