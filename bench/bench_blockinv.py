@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Latency of the batched candidate-block inversion (pivot search) in isolation (device-side events).
 
-    [BI_M="64 128"] [BI_NBLK="8 32 64 256"] python bench/bench_blockinv.py [panel] [panel_rl] [panel1] [sweep]
+    [BI_M="64 128"] [BI_NBLK="8 32 64 256"] python bench/bench_blockinv.py [panel] [sweep] [co] [generic]
 """
 import json
 import os

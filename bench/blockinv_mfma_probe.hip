@@ -7,7 +7,7 @@
 #include <random>
 #include <vector>
 
-template <int MP, int RL>
+template <int MP, int LAY>
 static void run(int m, int nblk) {
   using namespace gj::kern;
   std::vector<double> h((size_t)m * nblk * m);
@@ -23,13 +23,12 @@ static void run(int m, int nblk) {
   (void)hipMalloc(&used, nblk * 4);
   (void)hipMemset(used, 0, nblk * 4);
   (void)hipMemcpy(Lt, h.data(), h.size() * 8, hipMemcpyHostToDevice);
-  const int NW = MP / 16;
   for (int rep = 0; rep < 3; ++rep) {
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     (void)hipEventRecord(e0, 0);
-    hipLaunchKernelGGL((block_inverse_mfma_kernel<double, MP, RL>), dim3(nblk), dim3(64 * (NW + 1)), 0, 0, Lt,
+    hipLaunchKernelGGL((block_inverse_mfma_kernel<double, MP, LAY>), dim3(nblk), dim3(64 * bim_hw_waves<MP, LAY>()), 0, 0, Lt,
                        (int64_t)nblk * m, inv, scores, valid, used, m, (int64_t)1, (int64_t)0, 1e-12, nullptr);
     (void)hipEventRecord(e1, 0);
     (void)hipDeviceSynchronize();
@@ -40,36 +39,24 @@ static void run(int m, int nblk) {
     if (rep < 2) continue;
     const double t0 = (double)pr[1002];
     std::printf("%s m=%d nblk=%d: kernel %.1f us (event); shader cycles from wave-0 start:\n",
-                RL == 2 ? "pipelined" : RL == 1 ? "readlane-bcast" : "lds-bcast", m, nblk, ms * 1e3);
+                LAY == 1 ? "pivot-SIMD layout" : "9-wave layout", m, nblk, ms * 1e3);
     std::printf("  load done %.0f | pivot wave at B0(0) %.0f\n", pr[512] - t0, pr[0] - t0);
-    double steps = 0, aph = 0;
-    int nst = 0;
     for (int q = 0; q < m / 16; ++q) {
       const unsigned long long* P = pr + 8 + 24 * q;
-      aph += (double)(P[17] - P[0]);
-      std::printf("  panel %d: A start %.0f, 16 steps %.0f (", q, P[0] - t0, (double)(P[16] - P[0]));
-      for (int j = 0; j < 16; ++j) {
-        const double d = (double)(P[1 + j] - (j ? P[j] : P[0]));
-        std::printf("%s%.0f", j ? " " : "", d);
-        steps += d;
-        ++nst;
-      }
-      std::printf("), publish %.0f, B1 wait %.0f\n", (double)(P[17] - P[16]), (double)(P[18] - P[17]));
+      std::printf("  panel %d: pivot wave start %.0f, factor+publish %.0f, B1 wait %.0f\n", q, P[0] - t0,
+                  (double)(P[17] - P[0]), (double)(P[18] - P[17]));
       const unsigned long long* B = pr + 520 + 8 * q;
       std::printf("           block w0: apply %.0f, Xn %.0f, wait B1 %.0f, next tile %.0f, wait B0 %.0f\n",
                   (double)(B[1] - B[0]), (double)(B[2] - B[1]), (double)(B[3] - B[2]),
                   (double)(B[4] - B[3]), q + 1 < m / 16 ? (double)(B[8] - B[4]) : 0.0);
     }
-    std::printf("  A phase (steps + publish) per step %.0f cycles\n", aph / (16.0 * (m / 16)));
-    std::printf("  mean step %.0f cycles; epilogue (staged output + norm) %.0f; end %.0f\n", steps / nst,
-                (double)(pr[1001] - pr[1000]), pr[1001] - t0);
+    std::printf("  epilogue (staged output + norm) %.0f; end %.0f\n", (double)(pr[1001] - pr[1000]), pr[1001] - t0);
   }
 }
 
 int main() {
   run<128, 1>(128, 32);
-  run<128, 2>(128, 32);
-  run<64, 1>(64, 32);
-  run<64, 2>(64, 32);
+  run<128, 0>(128, 32);
+  run<64, 0>(64, 32);
   return 0;
 }

@@ -59,12 +59,10 @@ class Error : public std::runtime_error {
 // Stream roles.  MAIN runs the trailing (eliminate) update; SIDE runs the latency-critical
 // look-ahead work (pivot search + pivot-record exchange); COMM runs pivot-row normalisation and the
 // pivot-row broadcast.  Each RCCL communicator is bound to exactly one stream role.
-// S_MAIN2: second trailing-update stream; consecutive column chunks alternate between MAIN and
-// MAIN2 so that one chunk's GEMM tail overlaps the next chunk's ramp-up.
 // Hardware queues per process the engine needs (GPU_MAX_HW_QUEUES): one per stream, so that the
 // SIDE and COMM communicators' RCCL kernels never wait behind each other in one in-order queue.
 constexpr int kMinHwQueues = 16;
 
-enum StreamRole : int { S_MAIN = 0, S_SIDE = 1, S_COMM = 2, S_MAIN2 = 3, kNumStreams = 4 };
+enum StreamRole : int { S_MAIN = 0, S_SIDE = 1, S_COMM = 2, kNumStreams = 3 };
 
 }  // namespace gj

@@ -39,7 +39,9 @@ struct SolveOptions {
   DType dtype = DType::F64;
   int64_t chunk_cols = 0;   // pipelining granularity of the pivot-row broadcast (0 = auto)
   int depth = 0;            // elimination steps fused per trailing update (K = depth*m), 1..8;
-                            // 0 = auto: 2 up to N = 8192 (pivot-chain-bound), else 4
+                            // 0 = auto: 2 up to N = 8192 (pivot-chain-bound); 8 on ranks of
+                            // <= 4096 rows of a p > 1 job with N > 16384 (p = 8 at N = 32768);
+                            // else 4 (profiles/small_n_sweep.md, profiles/depth_pgt1.md)
   double eps = kDefaultEps;
   bool sync_debug = false;  // synchronise every stream after every phase (race screening)
   bool profile = false;     // per-phase device timers (HIP events) + roctx ranges
@@ -190,9 +192,6 @@ class Engine {
   int64_t panel_t0(int64_t v) const { return v * d_; }
   int64_t panel_q(int64_t v) const { return std::min<int64_t>(d_, L_.Nr - v * d_); }
   int64_t npanels() const { return (L_.Nr + d_ - 1) / d_; }
-  // trailing-update stream of column chunk c: with two_main_ chunks alternate between MAIN and
-  // MAIN2 so that one chunk's GEMM tail overlaps the next chunk's ramp-up (off by default)
-  int chunk_stream(int64_t c) const { return (two_main_ && (c & 1)) ? S_MAIN2 : S_MAIN; }
   // chunk c of the stacked-rows buffer: (d*m) x W block, ld W
   char* rb_chunk(int par, int64_t c) const {
     return elem(Rb_[par], (int64_t)d_ * L_.m * cb0_[c] * L_.m);
@@ -218,9 +217,8 @@ class Engine {
   // device buffers
   void* X_ = nullptr;       // input / working panel
   void* out_ = nullptr;     // result panel
-  // stacked K-major multipliers of a panel, (d*m) x rows, by panel index mod 3: with the trailing
-  // update split over two streams, panel u-2's last chunks may still read theirs while panel u's
-  // look-ahead writes panel u+1's
+  // stacked K-major multipliers of a panel, (d*m) x rows, by panel index mod 3 (panel u's chunks
+  // read theirs while the look-ahead of panel u writes panel u+1's and SIDE edits them)
   void* At_[3] = {nullptr, nullptr, nullptr};
   void* Rb_[2] = {nullptr, nullptr};   // stacked normalised pivot rows, chunk-major (d*m) x npad
   void* PP_[2] = {nullptr, nullptr};   // panel pieces: R_t restricted to the panel's columns, (d*m) x (d*m)
@@ -248,7 +246,7 @@ class Engine {
   PivotResult piv_[2][kMaxDepth];      // pivots of the panels in flight (by panel parity)
 
   // events
-  int ev_L_ = -1, ev_main_ = -1, ev_main2_ = -1, ev_sel_[2] = {-1, -1}, ev_edit_[2] = {-1, -1};
+  int ev_L_ = -1, ev_main_ = -1, ev_sel_[2] = {-1, -1}, ev_edit_[2] = {-1, -1};
   int ev_pp_[2][kMaxDepth] = {};
   std::vector<int> ev_c_;        // per chunk: MAIN finished the panel update of that chunk
   std::vector<int> ev_b_[2];     // per chunk: all stacked rows of that chunk broadcast
@@ -257,7 +255,6 @@ class Engine {
   struct PMark { int phase, ev0, ev1; };
   std::vector<PMark> pmarks_;
   bool solved_ = false;
-  bool two_main_ = false;
   // The work space did not fit on some rank (agreed at construction): solve() reports
   // Status::NoBlockMemory, the reference's "not enough memory for block" (main.cpp:428-436).
   bool block_mem_fail_ = false;

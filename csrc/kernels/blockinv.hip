@@ -277,296 +277,6 @@ __global__ __launch_bounds__(NTH) void block_inverse_kernel(const T* __restrict_
   }
 }
 
-// ---- panel-blocked variant (MP = 64/128): the latency chain runs inside ONE wave.
-//
-// The m sweep steps are grouped into panels of NB = 16 columns.  One Gauss-Jordan step with pivot
-// (r, kk) acts on every column x as  x <- x + u x[r]  (u_i = -a_ik/piv, u_r = 1/piv - 1) and replaces
-// column kk by u + e_r.  A panel's 16 steps therefore compose to  X <- X + U (E^T X)  on all other
-// columns (U: MP x 16 accumulated multipliers, E^T X: the 16 pivot rows before the panel), and
-// the panel's own columns end as U + E.  So:
-//   phase A  (wave 0 only, registers): 16 steps on the MP x 16 panel + U; pivot argmax by DPP /
-//            permlane wave max, pivot row by v_readlane (no LDS, no barrier inside a step);
-//   phase B  (all waves): rank-16 update of the other columns from U and the 16 pivot rows (LDS).
-// 3 workgroup barriers per panel instead of 2 per step.
-#ifdef GJ_BI_PROBE  // phase timestamps of workgroup 0 (bench/blockinv_probe.hip)
-__device__ unsigned long long g_bi_probe[256];
-#define BI_PROBE(slot)                                                            \
-  do {                                                                            \
-    if (blockIdx.x == 0 && threadIdx.x == 0) g_bi_probe[(slot)] = wall_clock64(); \
-  } while (0)
-#else
-#define BI_PROBE(slot) \
-  do {                 \
-  } while (0)
-#endif
-
-template <typename T, int MP, int NTH>
-__global__ __launch_bounds__(NTH) void block_inverse_panel_kernel(const T* __restrict__ Lt,
-                                                                  int64_t ldl,
-                                                                  T* __restrict__ inv_t,
-                                                                  double* __restrict__ scores,
-                                                                  int32_t* __restrict__ valid,
-                                                                  const int32_t* __restrict__ used,
-                                                                  int m, int64_t p, int64_t k,
-                                                                  double thresh) {
-  constexpr int NB = 16;          // steps per panel
-  constexpr int TY = NTH / 16;    // thread columns
-  constexpr int NA = MP / 16;     // rows per thread:    i = tx + 16 a
-  constexpr int NC = MP / TY;     // columns per thread: j = ty + TY c
-  constexpr int RPL = MP / 64;    // panel rows per lane of wave 0
-  static_assert(NC >= 1 && RPL >= 1 && TY % NB == 0, "bad geometry");
-
-  const int b = blockIdx.x;
-  const int64_t g = (int64_t)b * p + k;
-  if (used[g]) {
-    if (threadIdx.x == 0) {
-      valid[b] = 0;
-      scores[b] = 0.0;
-    }
-    return;
-  }
-  const int tid = threadIdx.x, lane = tid & 63, tx = tid & 15, ty = tid >> 4;
-
-  __shared__ T Pbuf[MP][NB + 1];
-  __shared__ T Ubuf[MP][NB + 1];
-  __shared__ T Rbuf[NB][MP];
-  __shared__ int prow[MP];
-  __shared__ int kinv[MP];
-  __shared__ int rsel[NB];
-  __shared__ int s_sing;
-  __shared__ double red[MP];
-  __shared__ double wmax[NTH / 64];
-  __shared__ T rowbuf[2][NB];
-
-  T w[NA][NC];
-#pragma unroll
-  for (int a = 0; a < NA; ++a) {
-    const int i = tx + 16 * a;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int j = ty + TY * c;
-      w[a][c] = (i < m && j < m) ? -Lt[(int64_t)j * ldl + (int64_t)b * m + i] : (i == j ? T(1) : T(0));
-    }
-  }
-  for (int i = tid; i < MP; i += NTH) red[i] = 0.0;
-  if (tid == 0) s_sing = 0;
-
-  for (int i = tid; i < MP; i += NTH) kinv[i] = -1;
-
-  bool usedr[RPL];  // wave 0: rows lane + 64 s already pivots
-#pragma unroll
-  for (int s = 0; s < RPL; ++s) usedr[s] = false;
-  bool sing = false;  // wave 0 (uniform)
-
-  // Pad steps (columns >= m) run too: their pivot is the pad row itself (identity) and they change
-  // nothing, which keeps every panel exactly NB steps long and the step code branch-free.
-  BI_PROBE(0);
-  for (int c0 = 0; c0 < m; c0 += NB) {
-    BI_PROBE(1 + 4 * (c0 / NB));
-    // (1) publish the panel columns c0 .. c0+15 (owners: threads whose ty covers them)
-    {
-      const int jj = ty - (c0 % TY);
-      if (jj >= 0 && jj < NB) {
-        const int cc = c0 / TY;
-#pragma unroll
-        for (int a = 0; a < NA; ++a) {
-          T v = T(0);
-#pragma unroll
-          for (int c = 0; c < NC; ++c)
-            if (c == cc) v = w[a][c];
-          Pbuf[tx + 16 * a][jj] = v;
-        }
-      }
-    }
-    __syncthreads();
-    BI_PROBE(2 + 4 * (c0 / NB));
-    // (2) phase A: wave 0 factors the panel.  The 16 steps are straight-line code (no branches, no
-    // LDS): the scheduler can run step j's non-critical updates under step j+1's argmax chain.
-    if (tid < 64) {
-      T P[RPL][NB], U[RPL][NB];
-#pragma unroll
-      for (int s = 0; s < RPL; ++s)
-#pragma unroll
-        for (int jj = 0; jj < NB; ++jj) {
-          P[s][jj] = Pbuf[lane + 64 * s][jj];
-          U[s][jj] = T(0);
-        }
-      int rr[NB];
-#pragma unroll
-      for (int jj = 0; jj < NB; ++jj) {
-        uint64_t key = 0;  // non-negative double keys order like their bit patterns
-#pragma unroll
-        for (int s = 0; s < RPL; ++s) {
-          const uint64_t kv =
-              usedr[s] ? 0 : __builtin_bit_cast(uint64_t, pivot_key(fabs((double)P[s][jj]), lane + 64 * s));
-          key = umax64(key, kv);
-        }
-        key = wave_max_u64(key);
-        const int r = __builtin_amdgcn_readfirstlane(255 - (int)(key & 0xFF));
-        const int rl = r & 63, rs = r >> 6;
-        rr[jj] = r;
-        // pivot row -> every lane through LDS (v_readlane is ~16 clk per dword and not pipelined;
-        // one masked ds_write + broadcast ds_read round trip is ~4x cheaper for 16 doubles)
-        T* rowb = rowbuf[jj & 1];
-#pragma unroll
-        for (int s = 0; s < RPL; ++s)
-          if (rs == s && lane == rl) {
-#pragma unroll
-            for (int kk = 0; kk < NB; ++kk) rowb[kk] = kk < jj ? U[s][kk] : P[s][kk];
-          }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        T rv[NB];
-#pragma unroll
-        for (int kk = 0; kk < NB; ++kk) rv[kk] = rowb[kk];
-        const T piv = rv[jj];
-        sing |= (c0 + jj < m) && !(fabs((double)piv) >= thresh);
-#pragma unroll
-        for (int s = 0; s < RPL; ++s) usedr[s] = usedr[s] || (s == rs && lane == rl);
-        // 1/piv: v_rcp_f64 + two Newton steps (the full division is a 10-op dependent chain)
-        T inv;
-        if constexpr (sizeof(T) == 8) {
-          inv = __builtin_amdgcn_rcp(piv);
-          inv = __builtin_fma(inv, __builtin_fma(-piv, inv, T(1)), inv);
-          inv = __builtin_fma(inv, __builtin_fma(-piv, inv, T(1)), inv);
-        } else {
-          inv = T(1) / piv;
-        }
-        T u[RPL];
-#pragma unroll
-        for (int s = 0; s < RPL; ++s) u[s] = (lane + 64 * s == r) ? inv - T(1) : -P[s][jj] * inv;
-        // critical path first: column jj+1 feeds the next argmax
-        if (jj + 1 < NB) {
-#pragma unroll
-          for (int s = 0; s < RPL; ++s) P[s][jj + 1] = __builtin_fma(u[s], rv[jj + 1], P[s][jj + 1]);
-        }
-#pragma unroll
-        for (int kk = 0; kk < NB; ++kk) {
-          if (kk == jj || kk == jj + 1) continue;
-#pragma unroll
-          for (int s = 0; s < RPL; ++s) {
-            if (kk < jj) U[s][kk] = __builtin_fma(u[s], rv[kk], U[s][kk]);
-            else P[s][kk] = __builtin_fma(u[s], rv[kk], P[s][kk]);
-          }
-        }
-#pragma unroll
-        for (int s = 0; s < RPL; ++s) U[s][jj] = u[s];
-      }
-#pragma unroll
-      for (int s = 0; s < RPL; ++s)
-#pragma unroll
-        for (int jj = 0; jj < NB; ++jj) Ubuf[lane + 64 * s][jj] = U[s][jj];
-      int myr = 0;
-#pragma unroll
-      for (int jj = 0; jj < NB; ++jj) myr = (lane == jj) ? rr[jj] : myr;
-      if (lane < NB) {
-        rsel[lane] = myr;
-        prow[c0 + lane] = myr;
-        kinv[myr] = c0 + lane;
-      }
-      if (sing && lane == 0) s_sing = 1;
-    }
-    __syncthreads();
-    BI_PROBE(3 + 4 * (c0 / NB));
-    if (s_sing) break;
-    // (3) the panel's pivot rows, as they were before the panel -> Rbuf
-#pragma unroll
-    for (int a = 0; a < NA; ++a) {
-      const int jj = kinv[tx + 16 * a] - c0;
-      if (jj >= 0 && jj < NB) {
-#pragma unroll
-        for (int c = 0; c < NC; ++c) Rbuf[jj][ty + TY * c] = w[a][c];
-      }
-    }
-    __syncthreads();
-    BI_PROBE(4 + 4 * (c0 / NB));
-    // (4) phase B: X += U * Rbuf on every column outside the panel; panel columns := U + E
-#pragma unroll
-    for (int k0 = 0; k0 < NB; k0 += 4) {
-      T uu[NA][4], rb[NC][4];
-#pragma unroll
-      for (int a = 0; a < NA; ++a)
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) uu[a][kk] = Ubuf[tx + 16 * a][k0 + kk];
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) rb[c][kk] = Rbuf[k0 + kk][ty + TY * c];
-#pragma unroll
-      for (int a = 0; a < NA; ++a)
-#pragma unroll
-        for (int c = 0; c < NC; ++c)
-#pragma unroll
-          for (int kk = 0; kk < 4; ++kk) w[a][c] = __builtin_fma(uu[a][kk], rb[c][kk], w[a][c]);
-    }
-    {
-      const int jj = ty - (c0 % TY);
-      if (jj >= 0 && jj < NB) {
-        const int cc = c0 / TY;
-        const int rj = rsel[jj];
-#pragma unroll
-        for (int a = 0; a < NA; ++a) {
-          const int i = tx + 16 * a;
-          const T v = Ubuf[i][jj] + (i == rj ? T(1) : T(0));
-#pragma unroll
-          for (int c = 0; c < NC; ++c)
-            if (c == cc) w[a][c] = v;
-        }
-      }
-    }
-  }
-
-  BI_PROBE(100);
-  if (s_sing) {
-    if (tid == 0) {
-      valid[b] = 0;
-      scores[b] = 0.0;
-    }
-    return;
-  }
-
-  // ||inv||_inf = max row abs-sum of the swept block (permutation invariant)
-#pragma unroll
-  for (int a = 0; a < NA; ++a) {
-    const int i = tx + 16 * a;
-    double s = 0.0;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int j = ty + TY * c;
-      if (j < m) s += fabs((double)w[a][c]);
-    }
-    if (i < m) atomicAdd(&red[i], s);
-  }
-  __syncthreads();
-  double mx = 0.0;
-  for (int i = tid; i < m; i += NTH) mx = fmax(mx, red[i]);
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off, 64));
-  if (lane == 0) wmax[tid >> 6] = mx;
-
-  // inverse, transposed: inv(W)[kinv[i]][prow[u]] = W_swept[i][u]
-  T* out = inv_t + (int64_t)b * m * m;
-#pragma unroll
-  for (int a = 0; a < NA; ++a) {
-    const int i = tx + 16 * a;
-    if (i >= m) continue;
-    const int ki = kinv[i];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int u = ty + TY * c;
-      if (u < m) out[(int64_t)prow[u] * m + ki] = w[a][c];
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    double sc = 0.0;
-    for (int q2 = 0; q2 < NTH / 64; ++q2) sc = fmax(sc, wmax[q2]);
-    scores[b] = sc;
-    valid[b] = isfinite(sc) ? 1 : 0;
-  }
-}
-
 // Generic path for m > 256: the working block lives in a global scratch area (one m*m slab per
 // workgroup), 256 threads.  Correct for any m; only used when the block exceeds the register path.
 template <typename T>
@@ -1017,9 +727,10 @@ static bool launch_blocked(const void* Lt, int64_t ldl, void* inv_t, double* sco
   return true;
 }
 
-// 0 = matrix-core panels (default), 1 = per-step sweep, 2 = one-wave panels, 3/4 = matrix-core
-// pivot-wave forms, 5 = co-resident L2-image kernel (fp64 32 < m <= 128; GJ_BI_VARIANT=co),
-// 6 = the per-step global sweep for m > 256 instead of the panel-blocked kernel (reference timing)
+// 0 = matrix-core panels (default: blockinv_mfma.hip for 16 < m <= 128, blockinv_big.hip for fp64
+// 128 < m <= 256, the panel-blocked kernel up to 1024), 1 = the per-step register sweep, 5 = the
+// co-resident L2-image kernel (fp64 32 < m <= 128; GJ_BI_VARIANT=co), 6 = the per-step global
+// sweep for m > 256 instead of the panel-blocked kernel (reference timing)
 static int g_bi_variant = -1;
 static int bi_variant() {
   if (g_bi_variant < 0) {
@@ -1043,20 +754,14 @@ static void launch_bi(const void* Lt, int64_t ldl, void* inv_t, double* scores, 
   if (g_bi_variant == 5 && block_inverse_co(sizeof(T) == 8 ? DType::F64 : DType::F32, Lt, ldl, inv_t, scores,
                                             valid, used, L, thresh, s, scratch))
     return;
-  if ((g_bi_variant == 0 || g_bi_variant == 3 || g_bi_variant == 4) &&
+  if (g_bi_variant == 0 &&
       block_inverse_mfma(sizeof(T) == 8 ? DType::F64 : DType::F32, Lt, ldl, inv_t, scores, valid, used,
-                         L, thresh, s, g_bi_variant == 0 ? 2 : g_bi_variant == 4 ? 1 : 0))
+                         L, thresh, s))
     return;
   if (g_bi_variant != 1 && block_inverse_big(sizeof(T) == 8 ? DType::F64 : DType::F32, Lt, ldl, inv_t, scores,
                                               valid, used, L, thresh, s, scratch))
     return;
-  if (g_bi_variant == 2 && m > 32 && m <= 64)
-    hipLaunchKernelGGL((block_inverse_panel_kernel<T, 64, 256>), dim3(grid), dim3(256), 0, s, lt, ldl,
-                       it, scores, valid, used, m, L.p, L.k, thresh);
-  else if (g_bi_variant == 2 && m > 64 && m <= 128)
-    hipLaunchKernelGGL((block_inverse_panel_kernel<T, 128, 512>), dim3(grid), dim3(512), 0, s, lt, ldl,
-                       it, scores, valid, used, m, L.p, L.k, thresh);
-  else if (m <= 32)
+  if (m <= 32)
     hipLaunchKernelGGL((block_inverse_kernel<T, 32, 256>), dim3(grid), dim3(256), 0, s, lt, ldl, it,
                        scores, valid, used, m, L.p, L.k, thresh, block_inverse_probe());
   else if (m <= 64)
@@ -1080,9 +785,8 @@ const char* block_inverse_kernel_name(DType dt, int64_t m, int variant) {
   const int v = variant >= 0 ? variant : bi_variant();
   const bool f64 = dt == DType::F64;
   if (v == 5 && f64 && m > 32 && m <= 128) return "l2_coresident";
-  if ((v == 0 || v == 3 || v == 4) && m > 16 && m <= 128) return "mfma_register";
+  if (v == 0 && m > 16 && m <= 128) return "mfma_register";
   if (v != 1 && f64 && m > 128 && m <= 256) return "l2_image";
-  if (v == 2 && m > 32 && m <= 128) return "panel_one_wave";
   if (m <= 128 || (m <= 256 && !f64)) return "register_sweep";
   if (v != 6 && m <= 1024) return "panel_blocked";
   return "generic";

@@ -307,15 +307,10 @@ bool block_inverse_big(DType dt, const void* Lt, int64_t ldl, void* inv_t, doubl
   if (dt != DType::F64 || m <= 128 || m > 256) return false;
   const unsigned grid = (unsigned)L.nblk;
   if (grid == 0) return true;
-  static const int lay = getenv("GJ_BI_LAYOUT") ? atoi(getenv("GJ_BI_LAYOUT")) : 1;
-  if (lay == 1)
-    hipLaunchKernelGGL((block_inverse_l2_kernel<256, 8, 1>), dim3(grid), dim3(64 * 11), 0, s,
-                       static_cast<const double*>(Lt), ldl, static_cast<double*>(inv_t), scores, valid, used, m,
-                       L.p, L.k, thresh, static_cast<double*>(scratch), block_inverse_probe());
-  else
-    hipLaunchKernelGGL((block_inverse_l2_kernel<256, 8>), dim3(grid), dim3(64 * 9), 0, s,
-                       static_cast<const double*>(Lt), ldl, static_cast<double*>(inv_t), scores, valid, used, m,
-                       L.p, L.k, thresh, static_cast<double*>(scratch), block_inverse_probe());
+  // the pivot wave alone on its SIMD (11-wave layout): -6 to -7 % per batch against the 9-wave one
+  hipLaunchKernelGGL((block_inverse_l2_kernel<256, 8, 1>), dim3(grid), dim3(64 * 11), 0, s,
+                     static_cast<const double*>(Lt), ldl, static_cast<double*>(inv_t), scores, valid, used, m,
+                     L.p, L.k, thresh, static_cast<double*>(scratch), block_inverse_probe());
   return true;
 }
 

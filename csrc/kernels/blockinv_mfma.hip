@@ -40,9 +40,6 @@
 namespace gj {
 namespace kern {
 
-#ifndef GJ_BI_EXP  // timing experiments only (bench/blockinv_mfma_probe.hip): bit 0 = skip the
-#define GJ_BI_EXP 0   // off-chain updates, bit 1 = fixed pivot row, bit 2 = no reciprocal refinement
-#endif
 #ifdef GJ_BI_PROBE  // shader-clock stamps of workgroup 0 (bench/blockinv_mfma_probe.hip)
 __device__ unsigned long long g_bim_probe[1024];
 #define BIM_PROBE(slot)                                                                       \
@@ -90,7 +87,7 @@ struct BiTile<float> {
 template <int MP, int LAY>
 constexpr int bim_hw_waves() { return MP / 16 + 1 + (LAY ? (MP / 16 - 1) / 3 : 0); }
 
-template <typename T, int MP, int PV, int LAY = 0>
+template <typename T, int MP, int LAY = 0>
 __global__ __launch_bounds__(64 * (MP / 16 + 1 + (LAY ? (MP / 16 - 1) / 3 : 0))) void block_inverse_mfma_kernel(
     const T* __restrict__ Lt, int64_t ldl, T* __restrict__ inv_t, double* __restrict__ scores,
     int32_t* __restrict__ valid, const int32_t* __restrict__ used, int m, int64_t p, int64_t k,
@@ -126,7 +123,6 @@ __global__ __launch_bounds__(64 * (MP / 16 + 1 + (LAY ? (MP / 16 - 1) / 3 : 0)))
   T(*Xn)[LDR] = reinterpret_cast<T(*)[LDR]>(big + 3 * MP * LDR);
   T* S = big;
   __shared__ T Rw[NW][16][16];   // per block wave: the current panel's pivot rows over its columns
-  __shared__ __attribute__((aligned(16))) T rowb[2][RPL][16];  // pivot wave: pivot-row broadcast
   __shared__ int rsel[2][16];    // pivot rows of the last two panels
   __shared__ int prow[MP];       // prow[c] = pivot row of column c
   __shared__ int kinv[MP];       // kinv[r] = column pivoted on row r (-1 = not yet)
@@ -188,81 +184,7 @@ __global__ __launch_bounds__(64 * (MP / 16 + 1 + (LAY ? (MP / 16 - 1) / 3 : 0)))
         for (int jj = 0; jj < 16; ++jj) W[s][jj] = (lane + 64 * s < MP) ? Pb[lane + 64 * s][jj] : T(0);
       int rr[16];
       bool sing = false;
-      if constexpr (PV == 2) {
-        pivot_panel_il<T, RPL>(W, keymask, pos, lane, c0, m, thresh, rr, sing);
-      } else {
-#pragma unroll
-      for (int jj = 0; jj < 16; ++jj) {
-        // keys: |value| bits, 0 for rows already pivots (a NaN can win: that block is singular,
-        // |piv| >= thresh fails, as its norm would be NaN)
-        uint64_t mag[RPL];
-#pragma unroll
-        for (int s = 0; s < RPL; ++s) mag[s] = __builtin_bit_cast(uint64_t, (double)W[s][jj]) & keymask[s];
-        bool none;
-        int r;
-        if constexpr ((GJ_BI_EXP & 2) != 0) {
-          r = c0 + jj;
-          none = false;
-        } else {
-          r = wave_pivot_row_u64<RPL>(mag, none);
-        }
-        if (none) r = c0 + jj;  // nothing left to choose (singular): any in-range row
-        r = __builtin_amdgcn_readfirstlane(r);
-        rr[jj] = r;
-        const int rl = r & 63, rs = r >> 6;
-        // the pivot value and the next column's entry (the next step's chain) by v_readlane; the
-        // rest of the pivot row (its values before this step) by v_readlane too (RLB: scalar
-        // operands of the updates) or through LDS
-        const T piv = readlane_t(RPL > 1 && rs ? W[RPL - 1][jj] : W[0][jj], rl);
-        const T nx = jj + 1 < 16 ? readlane_t(RPL > 1 && rs ? W[RPL - 1][jj + 1] : W[0][jj + 1], rl) : T(0);
-        sing |= (c0 + jj < m) && (none || !(fabs((double)piv) >= thresh));
-        T rv[16];
-        if constexpr (PV == 1) {
-          if (RPL > 1 && rs) {
-#pragma unroll
-            for (int kk = 0; kk < 16; ++kk)
-              if (kk != jj && kk != jj + 1) rv[kk] = readlane_t(W[RPL - 1][kk], rl);
-          } else {
-#pragma unroll
-            for (int kk = 0; kk < 16; ++kk)
-              if (kk != jj && kk != jj + 1) rv[kk] = readlane_t(W[0][kk], rl);
-          }
-        } else {
-          T* rb = &rowb[jj & 1][0][0];
-          if (lane == rl) {
-#pragma unroll
-            for (int s = 0; s < RPL; ++s)
-#pragma unroll
-              for (int kk = 0; kk < 16; ++kk) rb[16 * s + kk] = W[s][kk];
-          }
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-          for (int kk = 0; kk < 16; ++kk) rv[kk] = rb[16 * rs + kk];
-        }
-        const T inv = (GJ_BI_EXP & 4) ? __builtin_amdgcn_rcp(piv) : fast_recip(piv);
-        T u[RPL];
-#pragma unroll
-        for (int s = 0; s < RPL; ++s) u[s] = (lane + 64 * s == r) ? inv - T(1) : -W[s][jj] * inv;
-        if (jj + 1 < 16) {
-#pragma unroll
-          for (int s = 0; s < RPL; ++s) W[s][jj + 1] = __builtin_fma(u[s], nx, W[s][jj + 1]);
-        }
-#pragma unroll
-        for (int kk = 0; kk < 16; ++kk) {
-          if (kk == jj || kk == jj + 1 || (GJ_BI_EXP & 1)) continue;
-#pragma unroll
-          for (int s = 0; s < RPL; ++s) W[s][kk] = __builtin_fma(u[s], rv[kk], W[s][kk]);
-        }
-#pragma unroll
-        for (int s = 0; s < RPL; ++s) {
-          W[s][jj] = u[s];
-          if (lane + 64 * s == r) keymask[s] = 0ull;
-        }
-        BIM_PROBE(9 + 24 * q + jj);
-      }
-      }
+      pivot_panel_il<T, RPL>(W, keymask, pos, lane, c0, m, thresh, rr, sing);
       // publish U and the panel's pivot rows
 #pragma unroll
       for (int s = 0; s < RPL; ++s)
@@ -496,46 +418,28 @@ int32_t* block_inverse_probe() { return g_piv_probe; }
 
 bool block_inverse_mfma(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                         int32_t* valid, const int32_t* used, const Layout& L, double thresh,
-                        hipStream_t s, int pv) {
+                        hipStream_t s) {
   const int m = (int)L.m;
   if (m <= 16 || m > 128) return false;
   const unsigned grid = (unsigned)L.nblk;
   if (grid == 0) return true;
   const int MP = m <= 32 ? 32 : m <= 64 ? 64 : 128;
-  const dim3 blk(64 * (MP / 16 + 1));
-  // pivot wave alone on its SIMD (LAY 1) where the block waves' MFMAs would share it (MP = 128: 8
-  // block waves): 96.0 -> 86.4 us per batch of 64 fp64 128 x 128 candidates (MP = 64: no change);
-  // GJ_BI_LAYOUT=0 restores the 9-wave layout
-  static const int lay = getenv("GJ_BI_LAYOUT") ? atoi(getenv("GJ_BI_LAYOUT")) : 1;
-#define GJ_BI_LAUNCH1(T, MPV, PVV)                                                                    \
-  do {                                                                                                \
-    if (lay == 1 && PVV == 2 && MPV == 128)                                                           \
-      hipLaunchKernelGGL((block_inverse_mfma_kernel<T, MPV, PVV, 1>), dim3(grid),                     \
-                         dim3(64 * bim_hw_waves<MPV, 1>()), 0, s, static_cast<const T*>(Lt), ldl,     \
-                         static_cast<T*>(inv_t), scores, valid, used, m, L.p, L.k, thresh, g_piv_probe); \
-    else                                                                                              \
-      hipLaunchKernelGGL((block_inverse_mfma_kernel<T, MPV, PVV>), dim3(grid), blk, 0, s,              \
-                         static_cast<const T*>(Lt), ldl, static_cast<T*>(inv_t), scores, valid, used, \
-                         m, L.p, L.k, thresh, g_piv_probe);                                           \
-  } while (0)
-#define GJ_BI_LAUNCH(T, MPV)   \
-  if (pv == 2)                 \
-    GJ_BI_LAUNCH1(T, MPV, 2);  \
-  else if (pv == 1)            \
-    GJ_BI_LAUNCH1(T, MPV, 1);  \
-  else                         \
-    GJ_BI_LAUNCH1(T, MPV, 0)
+  // MP = 128: the pivot wave alone on its SIMD (LAY 1), where 8 block waves' MFMAs would share it:
+  // 96.0 -> 86.4 us per batch of 64 fp64 128 x 128 candidates (MP = 64: no change, 9-wave layout)
+#define GJ_BI_LAUNCH(T, MPV, LAYV)                                                                       \
+  hipLaunchKernelGGL((block_inverse_mfma_kernel<T, MPV, LAYV>), dim3(grid), dim3(64 * bim_hw_waves<MPV, LAYV>()), \
+                     0, s, static_cast<const T*>(Lt), ldl, static_cast<T*>(inv_t), scores, valid, used, m, L.p,   \
+                     L.k, thresh, g_piv_probe)
   if (dt == DType::F64) {
-    if (MP == 32) GJ_BI_LAUNCH(double, 32);
-    else if (MP == 64) GJ_BI_LAUNCH(double, 64);
-    else GJ_BI_LAUNCH(double, 128);
+    if (MP == 32) GJ_BI_LAUNCH(double, 32, 0);
+    else if (MP == 64) GJ_BI_LAUNCH(double, 64, 0);
+    else GJ_BI_LAUNCH(double, 128, 1);
   } else {
-    if (MP == 32) GJ_BI_LAUNCH(float, 32);
-    else if (MP == 64) GJ_BI_LAUNCH(float, 64);
-    else GJ_BI_LAUNCH(float, 128);
+    if (MP == 32) GJ_BI_LAUNCH(float, 32, 0);
+    else if (MP == 64) GJ_BI_LAUNCH(float, 64, 0);
+    else GJ_BI_LAUNCH(float, 128, 1);
   }
 #undef GJ_BI_LAUNCH
-#undef GJ_BI_LAUNCH1
   return true;
 }
 

@@ -139,7 +139,6 @@ struct GemmArgs {
   double* partial;  // [M][nparts]
   int nparts;
   bool latency;     // GemmExtra::latency -> CfgSmall for few-tile launches
-  int ablate;       // timing probe only (GJ_GEMM_ABLATE=1): no K-slice staging inside the loop
   int group;        // LDS-DMA kernel: tile rows per column-walk group (1 = row-major tile order)
 };
 
@@ -302,18 +301,18 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, const int tile) {
   if (CF::PF == 1) {
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
-      if (kt + 1 < nk && !g.ablate) load_slice((int64_t)(kt + 1) * BK, S0{});
+      if (kt + 1 < nk ) load_slice((int64_t)(kt + 1) * BK, S0{});
       compute(cur);
-      if (kt + 1 < nk && !g.ablate) store_slice(cur ^ 1, S0{});
+      if (kt + 1 < nk ) store_slice(cur ^ 1, S0{});
       __syncthreads();
     }
   } else {
     // slice s lives in register slot s & 1: slice kt+2 is fetched while slice kt is multiplied
     // and slice kt+1 (fetched one iteration earlier) is written to the other LDS buffer.
     auto body = [&](int kt, auto ld_slot, auto st_slot) {
-      if (kt + 2 < nk && !g.ablate) load_slice((int64_t)(kt + 2) * BK, ld_slot);
+      if (kt + 2 < nk ) load_slice((int64_t)(kt + 2) * BK, ld_slot);
       compute(kt & 1);
-      if (kt + 1 < nk && !g.ablate) store_slice((kt & 1) ^ 1, st_slot);
+      if (kt + 1 < nk ) store_slice((kt & 1) ^ 1, st_slot);
       __syncthreads();
     };
     for (int kt = 0; kt < nk; kt += 2) {
@@ -394,7 +393,7 @@ __global__ __launch_bounds__(CF::NT, CF::WAVES_PER_SIMD) void gemm_batch_kernel(
 // 8-deep slice (two A rows, then two B rows) into an NS-stage LDS ring, and the only waits in the
 // loop are a counted vmcnt and a raw s_barrier.  Freeing the staging registers lets five
 // workgroups share a CU.  Measured at 32768 x 4096 x 512: 62.6 TF/s (register staging 57.6; the
-// same tile with no staging at all — GJ_GEMM_ABLATE — 66.8).  Masked elements come back as zeros
+// same tile with no staging at all, a round-2 timing probe, 66.8).  Masked elements come back as zeros
 // from out-of-range buffer offsets.
 // LDS images: A [k][128 + 16 pad] (one DMA piece = one k row); B [k][64] with the two 128-B halves
 // of every odd row swapped (element n of row k at n ^ 16(k&1)), so the four k rows read by one
@@ -599,222 +598,16 @@ static void launch_glds(const GemmArgs& a0, hipStream_t s) {
   // ("2") 61.2, <2,3,8> ("9") 60.5; 3/4/5 stages 59.4/59.1/53.7.  Inside the solver the order
   // flips: N=32768 <2,3,8> 1138 ms, <2,4,8> 1147, <2,5,8> 1205 (profiles/cu_reserve_sweep.md,
   // profiles/gemm_variants_k512.md): at 4 workgroups per CU the pivot-path kernels find room, and
-  // the <2,3,8> schedule is the faster of the two 4-per-CU builds, so it is the default.  Tile rows
-  // are walked in groups of 4 (+0.5-1 %).
-  static const int stages = getenv("GJ_GLDS_STAGES") ? atoi(getenv("GJ_GLDS_STAGES")) : 9;
-  static const int group = getenv("GJ_GEMM_GROUP") ? atoi(getenv("GJ_GEMM_GROUP")) : 4;
-  a.group = group;
-  const dim3 grid((unsigned)nwg), blk(glds::NT);
-  switch (stages) {  // LDS per workgroup: 13.3 KiB per stage
-    case 2: hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 4, 8>), grid, blk, 0, s, a); break;  // 4 WG/CU
-    default: hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 3, 8>), grid, blk, 0, s, a); break;  // 3 WG/CU
-  }
+  // the <2,3,8> schedule is the faster of the two 4-per-CU builds, so it is the only build.  Tile
+  // rows are walked in groups of 4 (+0.5-1 %; groups 1-32 measured).
+  a.group = 4;
+  hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 3, 8>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
 }
 
 static bool glds_ok(const GemmArgs& a) {
   const auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   return a.M % 2 == 0 && a.N % 2 == 0 && a.lda % 2 == 0 && a.ldb % 2 == 0 && al16(a.A) && al16(a.B) &&
          a.lda * a.K * 8 < kRecords && a.ldb * a.K * 8 < kRecords && a.ldc * 128 * 8 < kRecords;
-}
-
-// ---- fp64 trailing update with the A operand straight to VGPRs (GJ_GEMM_VARIANT=dtva).
-//
-// 128 x 128 tile, 4 waves of 32 x 128.  A wave's 32 tile rows are its own, so its A fragments go
-// global -> VGPR (one 16-byte load per lane per 4-deep k step, issued PG slices ahead) and never
-// touch LDS; only B (16 x 128 per slice, read by all four waves) goes through a 2-stage LDS-DMA
-// ring, 4 one-KiB pieces per wave per slice.  A 16-byte A load gives a lane two consecutive tile
-// rows of one k, so MFMA row tile t holds tile rows 32 w + 2 i + t (i = the instruction's row);
-// the C map follows that permutation.  Per 16-deep slice a wave issues 64 MFMAs, 32 ds_read_b64
-// (0.5 per MFMA; 0.75 in the 128 x 64 kernel) and meets one barrier.  ~200 VGPRs: 2 per CU.
-// B image as in gemm_glds_f64: row k at [k][128], the 128-B halves of odd rows swapped.
-namespace dtva {
-constexpr int BM = 128, BN = 128, BK = 16, NT = 256;
-constexpr int SB = BK * BN;  // doubles per B stage
-}  // namespace dtva
-
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-// s_waitcnt vmcnt(n) for n in {0, 4, 8, 12} (rounded down: waiting for more is always safe)
-__device__ __forceinline__ void vm_wait4(int n) {
-  if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-template <int MODE, int PG>
-__global__ __launch_bounds__(dtva::NT, 2) void gemm_dtva_f64(GemmArgs g) {
-  using namespace dtva;
-  using MF = Mfma<double>;
-  using acc_t = MF::acc_t;
-  static_assert(PG == 1 || PG == 2, "A slices in flight");
-  constexpr int ES = 8, NJ = BN / 16, NA = PG + 1;
-  __shared__ double lds[2 * SB];
-
-  const int nwg = g.tiles_m * g.tiles_n;
-  const int tile = xcd_remap((int)blockIdx.x, nwg);
-  const int G = g.group > 0 ? g.group : 1;
-  const int grp = tile / (G * g.tiles_n), gr0 = grp * G;
-  const int gsz = (g.tiles_m - gr0) < G ? (g.tiles_m - gr0) : G;
-  const int rem = tile - grp * G * g.tiles_n;
-  const int tm = gr0 + rem % gsz, tn = rem / gsz;
-  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const double* A = static_cast<const double*>(g.A);
-  const double* B = static_cast<const double*>(g.B);
-  double* C = static_cast<double*>(g.C);
-  const int ldc = (int)g.ldc, ldb = (int)g.ldb, lda = (int)g.lda;
-  const int cl = lane & 15;
-
-  const int Mt = (int)((g.M - m0) < BM ? (g.M - m0) : BM);
-  const int Nt = (int)((g.N - n0) < BN ? (g.N - n0) : BN);
-  const int64_t zlo = g.zc0 - n0, zhi = g.zc1 - n0;
-  const int z0 = (int)(zlo < 0 ? 0 : (zlo > BN ? BN : zlo)), z1 = (int)(zhi < 0 ? 0 : (zhi > BN ? BN : zhi));
-  int zr0[GemmExtra::kMaxZeroRows], zr1[GemmExtra::kMaxZeroRows];
-#pragma unroll
-  for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) {
-    const int64_t lo = g.zr[z] - m0, hi = g.zr[z] + g.zh - m0;
-    zr0[z] = (int)(lo < 0 ? 0 : (lo > BM ? BM : lo));
-    zr1[z] = (int)(hi < 0 ? 0 : (hi > BM ? BM : hi));
-  }
-  // accumulator (t, j, q) of lane l: tile row rbase + 8 q + t, column 16 j + (l & 15)
-  __amdgpu_buffer_rsrc_t rc = rsrc(C + m0 * g.ldc + n0);
-  const int rbase = 32 * wid + 2 * (lane >> 4);
-  const int cvoff = (rbase * ldc + cl) * ES;
-  acc_t acc[2][NJ];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = rbase + 8 * q + t;
-      const int soff = (8 * q + t) * ldc * ES;
-      bool zrow = false;
-#pragma unroll
-      for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) zrow |= (r >= zr0[z] && r < zr1[z]);
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int c = cl + 16 * j;
-        if (MODE == MODE_ACC) {
-          const bool ok = r < Mt && c < Nt && !zrow && !(c >= z0 && c < z1);
-          acc[t][j][q] = bload<double>(rc, ok ? cvoff + j * 16 * ES : kOOB, soff);
-        } else {
-          acc[t][j][q] = 0.0;
-        }
-      }
-    }
-  // C must have landed before the first LDS-DMA is counted by the hand-written waits below
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) asm volatile("" ::"v"(acc[t][j][q]));
-
-  const int Kd = (int)g.K;
-  // A: lane l -> k row (l >> 4) of each 4-deep step, tile rows 32 w + 2 (l & 15) + {0, 1}
-  const int arow = 32 * wid + 2 * cl;
-  const bool a_ok = (m0 + arow) < g.M;  // M even: both rows or neither
-  __amdgpu_buffer_rsrc_t ra = rsrc(A + m0);
-  const int avoff = ((lane >> 4) * lda + arow) * ES;
-  // B: wave w moves slice rows w + 4 h; lane l -> LDS doubles 2 l, 2 l + 1 of the row
-  __amdgpu_buffer_rsrc_t rb = rsrc(B + n0);
-  const int bcol = (2 * lane) ^ ((wid & 1) * 16);
-  const bool b_ok = (n0 + bcol) < g.N;
-
-  u32x4 areg[NA][4];
-  auto issueA = [&](int kt, u32x4(&dst)[4]) {
-    const int k0 = kt * BK;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const bool ok = a_ok && (k0 + 4 * ks + (lane >> 4)) < Kd;
-      dst[ks] = __builtin_amdgcn_raw_buffer_load_b128(ra, ok ? avoff : kOOB, (k0 + 4 * ks) * lda * ES, 0);
-    }
-  };
-  auto issueB = [&](int kt) {
-    double* st = lds + (kt & 1) * SB;
-    const int k0 = kt * BK;
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const int kr = wid + 4 * h;
-      const bool ok = b_ok && (k0 + kr) < Kd;
-      dma16(rb, st + kr * BN, ok ? ((k0 + kr) * ldb + bcol) * ES : kOOB);
-    }
-  };
-  auto compute = [&](int kt, const u32x4(&a)[4]) {
-    const double* sb = lds + (kt & 1) * SB;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const int kr = 4 * ks + (lane >> 4);
-      const int sw = (kr & 1) * 16;
-      double b[NJ];
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) b[j] = sb[kr * BN + ((16 * j + cl) ^ sw)];
-      const double a0 = __builtin_bit_cast(double, u32x2{a[ks][0], a[ks][1]});
-      const double a1 = __builtin_bit_cast(double, u32x2{a[ks][2], a[ks][3]});
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        acc[0][j] = MF::op(a0, b[j], acc[0][j]);
-        acc[1][j] = MF::op(a1, b[j], acc[1][j]);
-      }
-    }
-  };
-
-  const int nk = (int)((g.K + BK - 1) / BK);
-  // issue order: B(0), A(0) .. A(PG-1); then body kt issues B(kt+1), A(kt+PG)
-  issueB(0);
-  issueA(0, areg[0]);
-  if (PG == 2 && nk > 1) issueA(1, areg[1]);
-  vm_wait4(4 * ((PG == 2 && nk > 1) ? 2 : 1));  // B(0) landed (A is waited for by the compiler)
-  __builtin_amdgcn_s_barrier();
-  auto body = [&](auto P, int kt) {
-    constexpr int p = decltype(P)::value;
-    const bool nb = kt + 1 < nk, na = kt + PG < nk;
-    if (nb) issueB(kt + 1);
-    if (na) issueA(kt + PG, areg[(p + PG) % NA]);
-    compute(kt, areg[p]);
-    if (nb) {
-      vm_wait4(na ? 4 : 0);  // B(kt+1) landed; A(kt+PG) may stay in flight
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-  };
-  int kt = 0;
-  for (; kt + NA <= nk; kt += NA) {
-    body(std::integral_constant<int, 0>{}, kt);
-    body(std::integral_constant<int, 1>{}, kt + 1);
-    if constexpr (NA == 3) body(std::integral_constant<int, 2>{}, kt + 2);
-  }
-  if (kt < nk) body(std::integral_constant<int, 0>{}, kt);
-  if (kt + 1 < nk) body(std::integral_constant<int, 1>{}, kt + 1);
-
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = rbase + 8 * q + t;
-      const int soff = (8 * q + t) * ldc * ES;
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int c = cl + 16 * j;
-        bstore(acc[t][j][q], rc, (r < Mt && c < Nt) ? cvoff + j * 16 * ES : kOOB, soff);
-      }
-    }
-}
-
-template <int MODE>
-static void launch_dtva(const GemmArgs& a0, hipStream_t s) {
-  GemmArgs a = a0;
-  a.tiles_m = (int)((a.M + dtva::BM - 1) / dtva::BM);
-  a.tiles_n = (int)((a.N + dtva::BN - 1) / dtva::BN);
-  const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;
-  if (nwg <= 0) return;
-  static const int pg = getenv("GJ_DTVA_PG") ? atoi(getenv("GJ_DTVA_PG")) : 2;
-  static const int group = getenv("GJ_GEMM_GROUP") ? atoi(getenv("GJ_GEMM_GROUP")) : 4;
-  a.group = group;
-  const dim3 grid((unsigned)nwg), blk(dtva::NT);
-  if (pg == 1) hipLaunchKernelGGL((gemm_dtva_f64<MODE, 1>), grid, blk, 0, s, a);
-  else hipLaunchKernelGGL((gemm_dtva_f64<MODE, 2>), grid, blk, 0, s, a);
 }
 
 // ---- fp32 trailing-update GEMM: the same LDS-DMA ring, built around v_mfma_f32_32x32x2_f32.
@@ -1001,22 +794,13 @@ static void launch_glds32(const GemmArgs& a0, hipStream_t s) {
   a.tiles_n = (int)((a.N + glds32::BN - 1) / glds32::BN);
   const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;
   if (nwg <= 0) return;
-  static const int cfg = getenv("GJ_GLDS32") ? atoi(getenv("GJ_GLDS32")) : 0;
-  static const int group = getenv("GJ_GEMM_GROUP") ? atoi(getenv("GJ_GEMM_GROUP")) : 4;
-  a.group = group;
-  const dim3 grid((unsigned)nwg), blk(glds32::NT);
+  a.group = 4;
   // <stages, launch-bounds workgroups per CU, slice depth>; 8 KiB of LDS per 8 k rows.  Measured
-  // (scripts/f32_ab.sh, TF/s at 32768x16384x512 / 16384x65536x512 / 4096x65536x1024): <2,3,16>
+  // (round 2, TF/s at 32768x16384x512 / 16384x65536x512 / 4096x65536x1024): <2,3,16>
   // 125.9 / 128.5 / 132.4 (4 WG/CU at 114 VGPRs), <2,2,16> 122.1 / 128.1 / 133.1, <3,2,16> 122.5 /
   // 125.0 / 129.1, <2,3,8> 125.3 / 127.7 / 131.4, <2,2,32> 116.2 / 118.4 / 124.1; squarepf 117.8 /
   // 119.8 / 122.3.
-  switch (cfg) {
-    case 1: hipLaunchKernelGGL((gemm_glds_f32<MODE, 2, 2, 16>), grid, blk, 0, s, a); break;
-    case 2: hipLaunchKernelGGL((gemm_glds_f32<MODE, 3, 2, 16>), grid, blk, 0, s, a); break;
-    case 3: hipLaunchKernelGGL((gemm_glds_f32<MODE, 2, 3, 8>), grid, blk, 0, s, a); break;
-    case 4: hipLaunchKernelGGL((gemm_glds_f32<MODE, 2, 2, 32>), grid, blk, 0, s, a); break;
-    default: hipLaunchKernelGGL((gemm_glds_f32<MODE, 2, 3, 16>), grid, blk, 0, s, a); break;
-  }
+  hipLaunchKernelGGL((gemm_glds_f32<MODE, 2, 3, 16>), dim3((unsigned)nwg), dim3(glds32::NT), 0, s, a);
 }
 
 static bool glds32_ok(const GemmArgs& a) {
@@ -1048,7 +832,7 @@ static int gemm_variant() {
 }
 int gemm_variant_id(const char* name) {
   const std::string s(name);
-  static const char* names[] = {"big", "narrow", "", "", "", "", "squarepf", "", "", "bigpf", "auto", "glds", "dtva"};
+  static const char* names[] = {"big", "narrow", "", "", "", "", "squarepf", "", "", "bigpf", "auto", "glds"};
   for (int i = 0; i < (int)(sizeof(names) / sizeof(names[0])); ++i)
     if (*names[i] && s == names[i]) return i;
   return kAutoVariant;
@@ -1071,24 +855,15 @@ static void launch(const GemmArgs& a, hipStream_t s) {
     // kernel (61 TF/s vs 57.6 register-staged at 32768x4096x512), fp32 the 64x64-per-wave square
     // tile (110.5 TF/s).  Everything else keeps the register-staged narrow tile.
     const int64_t big_tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
-    static const int64_t min_k = getenv("GJ_GLDS_MINK") ? atoll(getenv("GJ_GLDS_MINK")) : 384;
-    const bool deep = a.K >= min_k && big_tiles >= 512;
-    static const bool deep_dtva = getenv("GJ_DEEP_DTVA") && atoi(getenv("GJ_DEEP_DTVA")) > 0;
-    v = !deep ? 1 : (deep_dtva ? 12 : 11);
-  }
-  if (v == 12) {  // A-direct fp64 kernel (candidate); anything it cannot take goes the auto way
-    if constexpr (sizeof(T) == 8 && AL == 1 && MODE != MODE_RESID) {
-      if (glds_ok(a)) return launch_dtva<MODE>(a, s);
-    }
-    v = 11;
+    const bool deep = a.K >= 384 && big_tiles >= 512;
+    v = deep ? 11 : 1;
   }
   if (v == 11) {  // LDS-DMA fp64 kernel; other dtypes / layouts / alignments take the next best tile
     if constexpr (sizeof(T) == 8 && AL == 1 && MODE != MODE_RESID) {
       if (glds_ok(a)) return launch_glds<MODE>(a, s);
     }
     if constexpr (sizeof(T) == 4 && AL == 1 && MODE != MODE_RESID) {
-      static const bool off = getenv("GJ_GLDS32") && atoi(getenv("GJ_GLDS32")) < 0;
-      if (!off && glds32_ok(a)) return launch_glds32<MODE>(a, s);
+      if (glds32_ok(a)) return launch_glds32<MODE>(a, s);
     }
     v = sizeof(T) == 8 ? 9 : 6;
   }
@@ -1107,8 +882,6 @@ static void fill_extra(GemmArgs& a, const GemmExtra* ex) {
   a.zh = ex ? ex->zh : 0;
   for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) a.zr[z] = (ex && z < ex->nzr) ? ex->zr[z] : kNone;
   a.latency = ex ? ex->latency : false;
-  static const int ablate = getenv("GJ_GEMM_ABLATE") ? atoi(getenv("GJ_GEMM_ABLATE")) : 0;
-  a.ablate = ablate;
 }
 
 void gemm(DType dt, int op, int a_kmajor, int64_t M, int64_t N, int64_t K, const void* A,

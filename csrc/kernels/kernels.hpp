@@ -20,7 +20,7 @@ void gemm_batch(DType dt, const GemmDesc* d, int n, hipStream_t s);
 int residual_nparts(int64_t N);
 int gemm_variant_id(const char* name);  // big | narrow | squarepf | bigpf | glds | auto
 void set_gemm_variant(int v);
-void set_block_inverse_variant(int v);  // 0/3/4 = matrix-core panels (pipelined / LDS / readlane row bcast), 1 = sweep, 2 = one-wave panels
+void set_block_inverse_variant(int v);  // 0 = default families, 1 = register sweep, 5 = co-resident, 6 = generic
 int block_inverse_variant();
 const char* block_inverse_kernel_name(DType dt, int64_t m, int variant);
 void residual_partial(DType dt, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
@@ -34,7 +34,7 @@ void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* s
 // blockinv_mfma.hip: 16 < m <= 128 (false = not handled)
 bool block_inverse_mfma(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                         int32_t* valid, const int32_t* used, const Layout& L, double thresh,
-                        hipStream_t s, int pivot_variant /*0 LDS, 1 readlane, 2 pipelined*/);
+                        hipStream_t s);
 // test probe: when set, the matrix-core block inverses write the pivot row of every column of
 // every candidate to piv_out[b * m + c] (device memory; nullptr = off)
 void set_block_inverse_probe(int32_t* piv_out);

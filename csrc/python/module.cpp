@@ -163,12 +163,9 @@ PYBIND11_MODULE(_C, mod) {
   mod.def("set_block_inverse_variant", [](const std::string& v) {
     if (v == "panel") kern::set_block_inverse_variant(0);
     else if (v == "sweep") kern::set_block_inverse_variant(1);
-    else if (v == "panel1") kern::set_block_inverse_variant(2);
-    else if (v == "panel_lds") kern::set_block_inverse_variant(3);
-    else if (v == "panel_rl") kern::set_block_inverse_variant(4);
     else if (v == "co") kern::set_block_inverse_variant(5);
     else if (v == "generic") kern::set_block_inverse_variant(6);
-    else throw std::invalid_argument("block inverse variant: panel | sweep | panel1 | panel_lds | panel_rl | co | generic");
+    else throw std::invalid_argument("block inverse variant: panel | sweep | co | generic");
   });
   mod.def("set_block_inverse_probe", [](uintptr_t p) { kern::set_block_inverse_probe(reinterpret_cast<int32_t*>(p)); },
           "test probe: device int32 buffer (nblk x m) receiving each candidate's pivot row per column; 0 = off");

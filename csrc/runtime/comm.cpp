@@ -84,7 +84,7 @@ void Comm::note(int s, const char* kind, size_t bytes, int root) {
 }
 
 std::string Comm::last_op(int s) const {
-  static const char* names[kNumStreams] = {"MAIN", "SIDE", "COMM", "MAIN2"};
+  static const char* names[kNumStreams] = {"MAIN", "SIDE", "COMM"};
   if (s < 0 || s >= kNumStreams) return "?";
   return std::string(names[s]) + " stream, last collective " + (last_[s].empty() ? "none" : last_[s]);
 }

@@ -35,7 +35,7 @@ HipDevice::HipDevice(int device_index) : dev_(device_index) {
   HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
   for (int s = 0; s < kNumStreams; ++s) {
     hipStream_t st;
-    const int prio = (s == S_MAIN || s == S_MAIN2) ? lo : hi;
+    const int prio = (s == S_MAIN) ? lo : hi;
     HIP_OK(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, prio));
     streams_[s] = st;
   }
@@ -60,7 +60,7 @@ int HipDevice::reserve_cus(int n, int mode) {
   HIP_OK(hipGetDeviceProperties(&prop, dev_));
   const int ncu = prop.multiProcessorCount;
   n = std::max(0, std::min(n, ncu / 2));
-  for (int role : {S_MAIN, S_MAIN2}) {
+  for (int role : {S_MAIN}) {
     HIP_OK(hipStreamSynchronize(hs(streams_[role])));
     HIP_OK(hipStreamDestroy(hs(streams_[role])));
     hipStream_t st;

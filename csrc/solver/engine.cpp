@@ -112,7 +112,6 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // CU reservation for the latency-bound panel factorisation (GJ_RESERVE_CUS overrides).
   int rc = opt_.reserve_cus;
   if (const char* e = std::getenv("GJ_RESERVE_CUS")) rc = std::atoi(e);
-  if (const char* e = std::getenv("GJ_RESERVE_MODE")) opt_.reserve_mode = std::atoi(e);
   // auto: up to N = 16384 the pivot chain is the critical path and its block inverses only start
   // on a CU no trailing-update workgroup occupies, so keep 32 CUs (1/8 of the chip) off the MAIN
   // streams: N=8192 p=1 -12 %, emulated p=2/4/8 at N=16384 -10/-16/-14 %.  At N=32768 the GEMM is
@@ -166,17 +165,15 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
     const size_t pp_bytes = (size_t)L_.m * d_ * L_.m * esz();  // panel piece (SIDE, pivot chain)
     bcast_algo_ = comm_.tune_bcast(dev_, std::vector<size_t>{pp_bytes, (size_t)L_.m * wmax * esz()});
   }
-  // Two trailing-update streams (GJ_TWO_MAIN_STREAMS=1): measured slower — N=32768 1283 vs 1167 ms,
-  // p=8 emulation 0.191 vs 0.166 s (two concurrent GEMMs interleave their tiles, lose L2 locality
-  // and crowd out the pivot path) — so off by default.
-  if (const char* e = std::getenv("GJ_TWO_MAIN_STREAMS")) two_main_ = std::atoi(e) != 0;
+  // (One trailing-update stream: two alternating ones were measured slower, N=32768 1283 vs 1167 ms,
+  // p=8 emulation 0.191 vs 0.166 s -- concurrent GEMMs interleave their tiles, lose L2 locality and
+  // crowd out the pivot path -- and were removed in round 3.)
   // COMM chunk-normalisation GEMMs (m x chunk width x m) on the small 64x32 latency tile: 4x the
   // workgroups of the 128x64 tile.  Measured (profiles/small_n_sweep.md): N = 8192 30.2 -> 29.3 ms,
   // but N = 16384 +1.1 % and N = 32768 +0.7 % (more COMM workgroups beside the trailing update), so
   // only where the pivot chain dominates (padded order <= 8192).  GJ_COMM_SMALL_TILES overrides.
   comm_small_tiles_ = L_.npad <= 8192;
   if (const char* e = std::getenv("GJ_COMM_SMALL_TILES")) comm_small_tiles_ = std::atoi(e) != 0;
-  two_main_ = two_main_ && cb0_.size() > 1;
 
 }
 
@@ -279,7 +276,6 @@ void Engine::alloc_work(int64_t wmax) {
   if (ev_L_ >= 0) return;  // events are the device's; created once
   ev_L_ = dev_.create_event();
   ev_main_ = dev_.create_event();
-  ev_main2_ = dev_.create_event();
   for (int i = 0; i < 2; ++i) {
     ev_sel_[i] = dev_.create_event();
     ev_edit_[i] = dev_.create_event();
@@ -712,12 +708,11 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
   dbg_sync();
 }
 
-// MAIN streams: the depth-q trailing update of panel u.  The next panel's block columns are done
-// first (look-ahead) so its pivot search can start; then every other chunk.  Chunk c always runs on
-// chunk_stream(c), so chunk c of panel u+1 is ordered after chunk c of panel u by its stream alone,
-// and the two streams overlap one chunk's GEMM tail with the next chunk's ramp-up.  Hazards across
-// the streams: the multiplier panels are triple-buffered (At_[u % 3]); Rb_[par] chunk c is rewritten
-// by the COMM stream only after ev_c_[c] of the following panel (same stream as its readers).
+// MAIN stream: the depth-q trailing update of panel u.  The next panel's block columns are done
+// first (look-ahead) so its pivot search can start; then every other chunk, each behind the event
+// of its broadcast.  Hazards across streams: the multiplier panels are triple-buffered
+// (At_[u % 3]); Rb_[par] chunk c is rewritten by the COMM stream only after ev_c_[c] of the
+// following panel.
 void Engine::big_update(int64_t u) {
   const int par = (int)(u & 1);
   void* At = At_[u % 3];
@@ -728,11 +723,10 @@ void Engine::big_update(int64_t u) {
   const bool has_next = (u + 1 < npanels());
   const GemmExtra prows = pivot_rows_extra(par, q);
   dev_.wait(S_MAIN, ev_edit_[par]);
-  if (two_main_) dev_.wait(S_MAIN2, ev_edit_[par]);
   int64_t x0 = -1, x1 = -1;  // look-ahead columns
   if (has_next) {
     const int64_t tn = panel_t0(u + 1), qn = panel_q(u + 1), cn = chunk_of_[tn];
-    const int ms = chunk_stream(cn);
+    const int ms = S_MAIN;
     x0 = tn * m;
     x1 = (tn + qn) * m;
     dev_.wait(ms, ev_b_[par][cn]);
@@ -752,7 +746,7 @@ void Engine::big_update(int64_t u) {
   for (int64_t i = 0; i < C; ++i) {
     const int64_t c = (start + i) % C;
     const int64_t c0 = cb0_[c] * m, c1 = cb1_[c] * m, W = c1 - c0;
-    const int ms = chunk_stream(c);
+    const int ms = S_MAIN;
     dev_.wait(ms, ev_b_[par][c]);
     const int pe = prof_begin(ms);
     int64_t ra[2], rb[2], nr = 0;
@@ -845,10 +839,6 @@ SolveStats Engine::solve_steps() {
     return st;
   }
 
-  if (two_main_) {  // the last chunks may still run on MAIN2
-    dev_.record(ev_main2_, S_MAIN2);
-    dev_.wait(S_MAIN, ev_main2_);
-  }
   {
     cur_phase_ = "final exchange";
     const int pe = prof_begin(S_COMM);

@@ -1,6 +1,6 @@
 """HIP runtime settings the engine depends on, applied before the first HIP call of the process.
 
-* ``GPU_MAX_HW_QUEUES`` >= 16.  One process drives the engine's four streams (MAIN, MAIN2, SIDE,
+* ``GPU_MAX_HW_QUEUES`` >= 16.  One process drives the engine's three streams (MAIN, SIDE,
   COMM), torch's stream and, per RCCL communicator, RCCL's internal streams.  Streams beyond the
   HIP queue limit (default 4) SHARE a hardware queue, and a hardware queue executes in order.  The
   engine's progress argument for its two concurrently active RCCL communicators (SIDE: pivot

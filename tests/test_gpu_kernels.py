@@ -59,7 +59,7 @@ def test_extract_neg_t():
     assert torch.equal(Lt.cpu(), -X.cpu()[:, 128:224].t())
 
 
-@pytest.fixture(params=["panel", "sweep", "panel1", "co", "generic"])
+@pytest.fixture(params=["panel", "sweep", "co", "generic"])
 def bi_variant(request, native):
     native.set_block_inverse_variant(request.param)
     yield request.param
