@@ -58,6 +58,9 @@ def parse_args(argv=None):
     ap.add_argument("--depth", type=int, default=0,
                     help="elimination steps fused per trailing update (0 = the engine's choice)")
     ap.add_argument("--no-residual", action="store_true")
+    ap.add_argument("--pivot", choices=["block-min-inv-norm", "partial"], default="block-min-inv-norm",
+                    help="pivot rule: the reference's smallest ||inv(block)|| (the benchmarked algorithm) "
+                         "or block partial pivoting (a faster alternative mode)")
     ap.add_argument("--force-rccl", action="store_true", help="use the RCCL communicator even at 1 rank")
     ap.add_argument("--bcast", choices=["auto", "ring", "direct"], default=None,
                     help="pivot-row broadcast at p > 2 (default: GJ_BCAST or auto = both timed at "
@@ -208,7 +211,7 @@ def run_rank(args) -> int:
         # allocation is agreed on every rank inside the constructor (a rank that cannot allocate
         # makes every rank fail here, before any other collective)
         eng = C.Engine(dev, comm, args.n, args.m, args.dtype, args.chunk_cols, 1e-15, False, args.depth,
-                       args.profile, args.comm_timeout)
+                       args.profile, args.comm_timeout, args.pivot)
     except RuntimeError as e:
         return fail(e)
 
@@ -278,7 +281,8 @@ def run_rank(args) -> int:
                     + ("GPU" if gpu else "host (--device cpu rehearsal)") + " each step",
             "config": {
                 "model": f"dense block Gauss-Jordan inversion N={args.n} (block m={args.m}, in-place, "
-                         "min-inverse-norm block pivoting)",
+                         + ("min-inverse-norm block pivoting)" if args.pivot == "block-min-inv-norm"
+                            else "block partial pivoting)"),
                 "global_batch": 1,
                 "seq_len": args.n,
                 "parallelism": (f"block-row-cyclic p={world} (" +
@@ -302,6 +306,7 @@ def run_rank(args) -> int:
             "residual_inf": res,
             "status": st["status"],
             "offdiag_pivots": st["offdiag_pivots"],
+            "pivot_fallbacks": st.get("pivot_fallbacks", 0),
         }
         if args.same_gpu:
             out["same_gpu_rehearsal"] = True

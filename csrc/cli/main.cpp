@@ -22,7 +22,9 @@
 //   --print-max N        corner size (reference MAX_P = 10)
 //   --eps E              singularity threshold factor (reference EPS = 1e-15)
 //   --chunk-cols C       broadcast pipelining granularity
-//   --depth D            elimination steps fused per trailing update (1..8; default: 2 up to N=8192, else 4)
+//   --depth D            elimination steps fused per trailing update (1..8; default: engine.hpp)
+//   --pivot block-min-inv-norm|partial   pivot rule (default: the reference's smallest ||inv||;
+//                        partial = block partial pivoting, one candidate inverse per rank and step)
 //   --repeat R           time R solves, report the last (min also in --json)
 //   --out FILE           write the inverse (text, or .bin)
 //   --rhs ones|random|FILE  also solve A x = b (x = inv(A) b) and report ||A x - b||_inf
@@ -86,13 +88,13 @@ static void json_report(const RunConfig& cfg, const RunReport& rep) {
                "{\"n\": %lld, \"m\": %lld, \"ranks\": %d, \"device\": \"%s\", \"comm\": \"%s\", "
                "\"dtype\": \"%s\", \"status\": %d, \"glob_time\": %.6f, \"best_time\": %.6f, "
                "\"gflops_nominal\": %.3f, \"residual\": %.6e, \"residual_computed\": %s, "
-               "\"residual_fp64\": %s, \"host_wait_ms\": %.3f, \"offdiag_pivots\": %lld%s%s}\n",
+               "\"residual_fp64\": %s, \"host_wait_ms\": %.3f, \"offdiag_pivots\": %lld, \"pivot_fallbacks\": %lld%s%s}\n",
                (long long)cfg.n, (long long)cfg.m, cfg.ranks, rep.device_desc.c_str(),
                rep.comm_desc.c_str(), dtype_name(cfg.solve.dtype), (int)rep.status, rep.glob_time,
                rep.best_time, rep.gflops_nominal, rep.residual,
                rep.residual_computed ? "true" : "false", rep.residual_fp64 ? "true" : "false",
                rep.stats.host_wait_ms,
-               (long long)rep.stats.offdiag_pivots, phases.c_str(), rhs.c_str());
+               (long long)rep.stats.offdiag_pivots, (long long)rep.stats.pivot_fallbacks, phases.c_str(), rhs.c_str());
 }
 
 int main(int argc, char* argv[]) {
@@ -147,6 +149,12 @@ int main(int argc, char* argv[]) {
       else if (a == "--eps") cfg.solve.eps = std::atof(val("--eps"));
       else if (a == "--chunk-cols") cfg.solve.chunk_cols = std::atoll(val("--chunk-cols"));
       else if (a == "--depth") cfg.solve.depth = std::atoi(val("--depth"));
+      else if (a == "--pivot") {
+        const std::string pv = val("--pivot");
+        if (pv == "block-min-inv-norm") cfg.solve.pivot = PivotRule::MinInvNorm;
+        else if (pv == "partial") cfg.solve.pivot = PivotRule::Partial;
+        else return usage(argv[0]);
+      }
       else if (a == "--repeat") cfg.repeats = std::atoi(val("--repeat"));
       else if (a == "--out") out_file = val("--out");
       else if (a == "--rhs") cfg.rhs = val("--rhs");

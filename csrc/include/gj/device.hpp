@@ -145,6 +145,18 @@ class Device {
     return 0;
   }
   virtual void prepare_block_inverse(DType dt, const Layout& L, int variant) { (void)dt; (void)L; (void)variant; }
+  // Partial pivoting (SolveOptions::pivot = Partial, `--pivot partial`).  Every local candidate
+  // W_b (as in block_inverse) gets scores[b] = -max|W_b| and valid[b] = (max|W_b| >= thresh), so the
+  // common argmin (pivot_local) picks this rank's largest-magnitude candidate; its block alone is
+  // then copied out (gather_candidate: sel = K-major m x m, ld m; -I for an invalid record),
+  // inverted by block_inverse on a one-block layout, and commit_candidate stores that inverse in
+  // the candidate's slot of inv_t and clears rec->valid when the block is singular.
+  virtual void candidate_maxabs(DType dt, const void* Lt, int64_t ldl, double* scores, int32_t* valid,
+                                const int32_t* used, const Layout& L, double thresh, int s) = 0;
+  virtual void gather_candidate(DType dt, void* sel, const void* Lt, int64_t ldl, const PivotRec* rec,
+                                const Layout& L, int s) = 0;
+  virtual void commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1, PivotRec* rec,
+                                const Layout& L, int s) = 0;
   // Local argmin over this rank's candidates -> *out.
   virtual void pivot_local(const double* scores, const int32_t* valid, const int32_t* used,
                            const int32_t* pos, const Layout& L, PivotRec* out, int s) = 0;

@@ -35,6 +35,16 @@
 
 namespace gj {
 
+// Pivot rule of every step.
+//   MinInvNorm: the reference's rule (main.cpp:1039-1066): invert every candidate block, take the
+//               smallest ||inv||_inf (ties -> larger rank, then smaller local row).
+//   Partial:    block partial pivoting, a faster alternative: each rank takes its candidate with
+//               the largest-magnitude entry and inverts that block alone; among the ranks' records
+//               whose block is invertible the largest magnitude wins (same tie rule).  When every
+//               rank's choice is singular, that step falls back to the MinInvNorm search.  One
+//               candidate inverse per rank and step instead of one per candidate.
+enum class PivotRule : int { MinInvNorm = 0, Partial = 1 };
+
 struct SolveOptions {
   DType dtype = DType::F64;
   int64_t chunk_cols = 0;   // pipelining granularity of the pivot-row broadcast (0 = auto)
@@ -43,6 +53,7 @@ struct SolveOptions {
                             // <= 4096 rows of a p > 1 job with N > 16384 (p = 8 at N = 32768);
                             // else 4 (profiles/small_n_sweep.md, profiles/depth_pgt1.md)
   double eps = kDefaultEps;
+  PivotRule pivot = PivotRule::MinInvNorm;
   bool sync_debug = false;  // synchronise every stream after every phase (race screening)
   bool profile = false;     // per-phase device timers (HIP events) + roctx ranges
   double comm_timeout_s = 600;  // a host wait on a pivot longer than this is a peer failure
@@ -72,6 +83,7 @@ struct SolveStats {
   double host_wait_ms = 0;       // time the host spent blocked on pivot results
   std::vector<int32_t> pivots;   // physical pivot block row of every step
   int64_t offdiag_pivots = 0;    // steps whose pivot was not the "natural" row (needed a swap)
+  int64_t pivot_fallbacks = 0;   // PivotRule::Partial: steps that needed the MinInvNorm search
   double bcast_bytes = 0;        // bytes of pivot rows broadcast by this rank (as root)
   bool profiled = false;
   double phase_ms[kNumPhases] = {};   // SolveOptions::profile only
@@ -152,6 +164,7 @@ class Engine {
     int reserve_cus = 0;          // CUs kept off the trailing-update stream
     std::string block_inverse;    // candidate-inverse kernel
     bool comm_small_tiles = false;
+    std::string pivot;            // "block-min-inv-norm" | "partial"
   };
   Policy policy() const;
   const std::string& bcast_algo() const { return bcast_algo_; }  // "ring" | "direct"
@@ -164,7 +177,7 @@ class Engine {
   void free_work();     // everything but the matrix panels
   void free_buffers();
   // Pivot search for step t on the multiplier segment Lt (SIDE stream); result -> piv_host_[t&1].
-  void select(int64_t t, const void* Lt);
+  void select(int64_t t, const void* Lt, bool full = false);
   // Panel factorisation (pivot searches of its q steps, panel pieces, then the chunk pipeline of
   // the normalised pivot rows).  Returns false when the matrix is singular.
   bool factor_panel(int64_t v, bool wait_main, SolveStats& st, double& host_wait);
@@ -227,6 +240,14 @@ class Engine {
   void* T_ = nullptr;                  // row-update temp, m x Wmax
   void* RP_ = nullptr;                 // panel-piece temp, m x (d*m)
   void* inv_ = nullptr;
+  // PivotRule::Partial: the chosen candidate (K-major m x m), its inverse, score / validity, a zero
+  // "used" flag, and the one-block layout the inverse runs on
+  void* sel_ = nullptr;
+  void* inv1_ = nullptr;
+  double* score1_ = nullptr;
+  int32_t* valid1_ = nullptr;
+  int32_t* used1_ = nullptr;
+  Layout L1_;
   double* scores_ = nullptr;
   int32_t* valid_ = nullptr;
   int32_t* pos_ = nullptr;

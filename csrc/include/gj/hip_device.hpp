@@ -60,6 +60,12 @@ class HipDevice : public Device {
   void set_block_inverse_hint(int variant) override { bi_hint_ = variant; }
   size_t block_inverse_scratch_bytes(DType dt, const Layout& L, int variant) const override;
   void prepare_block_inverse(DType dt, const Layout& L, int variant) override;
+  void candidate_maxabs(DType dt, const void* Lt, int64_t ldl, double* scores, int32_t* valid,
+                        const int32_t* used, const Layout& L, double thresh, int s) override;
+  void gather_candidate(DType dt, void* sel, const void* Lt, int64_t ldl, const PivotRec* rec, const Layout& L,
+                        int s) override;
+  void commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1, PivotRec* rec,
+                        const Layout& L, int s) override;
   void pivot_local(const double* scores, const int32_t* valid, const int32_t* used,
                    const int32_t* pos, const Layout& L, PivotRec* out, int s) override;
   void pivot_select_single(const double* scores, const int32_t* valid, const Layout& L, int32_t t,

@@ -45,6 +45,12 @@ class HostDevice : public Device {
   void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                      int32_t* valid, const int32_t* used, const Layout& L, double thresh,
                      int s) override;
+  void candidate_maxabs(DType dt, const void* Lt, int64_t ldl, double* scores, int32_t* valid,
+                        const int32_t* used, const Layout& L, double thresh, int s) override;
+  void gather_candidate(DType dt, void* sel, const void* Lt, int64_t ldl, const PivotRec* rec, const Layout& L,
+                        int s) override;
+  void commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1, PivotRec* rec,
+                        const Layout& L, int s) override;
   void pivot_local(const double* scores, const int32_t* valid, const int32_t* used,
                    const int32_t* pos, const Layout& L, PivotRec* out, int s) override;
   void pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos, int32_t* phys_at,

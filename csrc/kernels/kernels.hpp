@@ -27,6 +27,14 @@ void residual_partial(DType dt, int64_t M, int64_t N, int64_t K, const void* A, 
                       const void* B, int64_t ldb, int64_t n_real, int64_t blk_m, int64_t p,
                       int64_t k, double* partial, hipStream_t s);
 
+// misc.hip: partial pivoting (SolveOptions::pivot = Partial)
+void candidate_maxabs(DType dt, const void* Lt, int64_t ldl, double* scores, int32_t* valid,
+                      const int32_t* used, const Layout& L, double thresh, hipStream_t s);
+void gather_candidate(DType dt, void* sel, const void* Lt, int64_t ldl, const PivotRec* rec, const Layout& L,
+                      hipStream_t s);
+void commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1, PivotRec* rec,
+                      const Layout& L, hipStream_t s);
+
 // blockinv.hip
 void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                    int32_t* valid, const int32_t* used, const Layout& L, double thresh,

@@ -14,6 +14,7 @@
 
 #include "gj/gen.hpp"
 #include "kernels.hpp"
+#include "wave_ops.hpp"
 
 namespace gj {
 namespace kern {
@@ -303,6 +304,108 @@ void pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos, int3
                   int32_t* used, int32_t* seq, PivotResult* out, PivotResult* host_out, hipStream_t s) {
   hipLaunchKernelGGL(pivot_global_kernel, dim3(1), dim3(64), 0, s, recs, p, t, pos, phys_at, used, seq,
                      out, host_out);
+}
+
+// ---------------------------------------------------------------- partial pivoting (--pivot partial)
+// Score of every local candidate block W_b = -(Lt block b)^T: its largest magnitude (scores[b] =
+// -max|W_b|, so the common argmin picks the largest), valid when that is >= thresh.  One
+// workgroup per block: each thread scans a strided part of the m x m block (K-major: column c of
+// W_b is the contiguous run Lt[c*ldl + b*m .. + m)).
+template <typename T>
+__global__ __launch_bounds__(256) void candidate_maxabs_kernel(const T* __restrict__ Lt, int64_t ldl, int m,
+                                                               int64_t p, int64_t k, double thresh,
+                                                               const int32_t* __restrict__ used,
+                                                               double* __restrict__ scores,
+                                                               int32_t* __restrict__ valid) {
+  const int b = blockIdx.x;
+  if (used[(int64_t)b * p + k]) {
+    if (threadIdx.x == 0) {
+      valid[b] = 0;
+      scores[b] = 0.0;
+    }
+    return;
+  }
+  double mx = 0.0;
+  const int64_t total = (int64_t)m * m;
+  for (int64_t e = threadIdx.x; e < total; e += blockDim.x) {
+    const int64_t c = e / m, i = e - c * m;
+    mx = fmax(mx, fabs((double)Lt[c * ldl + (int64_t)b * m + i]));
+  }
+  __shared__ double red[4];
+  mx = wave_max_f64(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) mx = fmax(mx, red[w]);
+    mx = fmax(mx, red[0]);
+    scores[b] = -mx;
+    valid[b] = (mx >= thresh && isfinite(mx)) ? 1 : 0;
+  }
+}
+
+void candidate_maxabs(DType dt, const void* Lt, int64_t ldl, double* scores, int32_t* valid,
+                      const int32_t* used, const Layout& L, double thresh, hipStream_t s) {
+  if (L.nblk <= 0) return;
+  if (dt == DType::F64)
+    hipLaunchKernelGGL(candidate_maxabs_kernel<double>, dim3((unsigned)L.nblk), dim3(256), 0, s,
+                       static_cast<const double*>(Lt), ldl, (int)L.m, L.p, L.k, thresh, used, scores, valid);
+  else
+    hipLaunchKernelGGL(candidate_maxabs_kernel<float>, dim3((unsigned)L.nblk), dim3(256), 0, s,
+                       static_cast<const float*>(Lt), ldl, (int)L.m, L.p, L.k, thresh, used, scores, valid);
+}
+
+// The chosen local candidate (rec, from pivot_local) copied out of Lt into sel (K-major m x m,
+// ld m: the single-block operand of block_inverse); an invalid record gives -I (W = I).
+template <typename T>
+__global__ __launch_bounds__(256) void gather_candidate_kernel(T* __restrict__ sel, const T* __restrict__ Lt,
+                                                               int64_t ldl, int m, int64_t p,
+                                                               const PivotRec* __restrict__ rec) {
+  const bool ok = rec->valid != 0;
+  const int64_t b = ok ? (int64_t)rec->phys / p : 0;
+  const int64_t total = (int64_t)m * m;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = e / m, i = e - c * m;
+    sel[e] = ok ? Lt[c * ldl + b * m + i] : (c == i ? T(-1) : T(0));
+  }
+}
+
+void gather_candidate(DType dt, void* sel, const void* Lt, int64_t ldl, const PivotRec* rec, const Layout& L,
+                      hipStream_t s) {
+  const unsigned grid = grid_for(L.m * L.m, 256, 64);
+  if (dt == DType::F64)
+    hipLaunchKernelGGL(gather_candidate_kernel<double>, dim3(grid), dim3(256), 0, s, static_cast<double*>(sel),
+                       static_cast<const double*>(Lt), ldl, (int)L.m, L.p, rec);
+  else
+    hipLaunchKernelGGL(gather_candidate_kernel<float>, dim3(grid), dim3(256), 0, s, static_cast<float*>(sel),
+                       static_cast<const float*>(Lt), ldl, (int)L.m, L.p, rec);
+}
+
+// After block_inverse on sel: the chosen candidate's slot of inv_t := inv1, and the record stays
+// valid only if that inverse exists (rec->valid &= valid1[0]).
+template <typename T>
+__global__ __launch_bounds__(256) void commit_candidate_kernel(T* __restrict__ inv_t, const T* __restrict__ inv1,
+                                                               const int32_t* __restrict__ valid1, int m,
+                                                               int64_t p, PivotRec* __restrict__ rec) {
+  const bool ok = rec->valid != 0 && valid1[0] != 0;
+  const int64_t b = (int64_t)rec->phys / p;
+  const int64_t total = (int64_t)m * m;
+  if (ok)
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x)
+      inv_t[b * total + e] = inv1[e];
+  __syncthreads();  // every thread has read rec before thread 0 of block 0 rewrites it
+  if (blockIdx.x == 0 && threadIdx.x == 0 && !ok) rec->valid = 0;
+}
+
+void commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1, PivotRec* rec,
+                      const Layout& L, hipStream_t s) {
+  // one workgroup: rec is read by every thread before thread 0 may clear it
+  if (dt == DType::F64)
+    hipLaunchKernelGGL(commit_candidate_kernel<double>, dim3(1), dim3(256), 0, s, static_cast<double*>(inv_t),
+                       static_cast<const double*>(inv1), valid1, (int)L.m, L.p, rec);
+  else
+    hipLaunchKernelGGL(commit_candidate_kernel<float>, dim3(1), dim3(256), 0, s, static_cast<float*>(inv_t),
+                       static_cast<const float*>(inv1), valid1, (int)L.m, L.p, rec);
 }
 
 // ---------------------------------------------------------------- owner edits (one launch)

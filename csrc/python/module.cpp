@@ -105,6 +105,12 @@ class PyComm : public Comm {
   int r_, n_;
 };
 
+PivotRule parse_pivot(const std::string& v) {
+  if (v == "block-min-inv-norm" || v == "min-inv-norm") return PivotRule::MinInvNorm;
+  if (v == "partial") return PivotRule::Partial;
+  throw std::invalid_argument("pivot: block-min-inv-norm | partial");
+}
+
 py::dict stats_to_dict(const SolveStats& st) {
   py::dict d;
   d["status"] = (int)st.status;
@@ -113,6 +119,7 @@ py::dict stats_to_dict(const SolveStats& st) {
   d["host_wait_ms"] = st.host_wait_ms;
   d["pivots"] = st.pivots;
   d["offdiag_pivots"] = st.offdiag_pivots;
+  d["pivot_fallbacks"] = st.pivot_fallbacks;
   d["bcast_bytes"] = st.bcast_bytes;
   if (st.profiled) {
     py::dict ph;
@@ -374,10 +381,11 @@ PYBIND11_MODULE(_C, mod) {
   py::class_<PyEngine>(mod, "Engine")
       .def(py::init([](std::shared_ptr<Device> dev, std::shared_ptr<Comm> comm, int64_t n, int64_t m,
                        const std::string& dtype, int64_t chunk_cols, double eps, bool sync_debug,
-                       int depth, bool profile, double comm_timeout_s) {
+                       int depth, bool profile, double comm_timeout_s, const std::string& pivot) {
              SolveOptions o;
              o.dtype = parse_dtype(dtype);
              o.depth = depth;
+             o.pivot = parse_pivot(pivot);
              o.profile = profile;
              o.comm_timeout_s = comm_timeout_s;
              o.chunk_cols = chunk_cols;
@@ -391,7 +399,8 @@ PYBIND11_MODULE(_C, mod) {
            }),
            py::arg("device"), py::arg("comm"), py::arg("n"), py::arg("m"), py::arg("dtype") = "fp64",
            py::arg("chunk_cols") = 0, py::arg("eps") = kDefaultEps, py::arg("sync_debug") = false,
-           py::arg("depth") = 0, py::arg("profile") = false, py::arg("comm_timeout_s") = 600.0)
+           py::arg("depth") = 0, py::arg("profile") = false, py::arg("comm_timeout_s") = 600.0,
+           py::arg("pivot") = "block-min-inv-norm")
       .def_property_readonly("layout",
                              [](PyEngine& e) {
                                const Layout& L = e.eng->layout();
@@ -413,6 +422,7 @@ PYBIND11_MODULE(_C, mod) {
                                d["reserve_cus"] = pl.reserve_cus;
                                d["block_inverse"] = pl.block_inverse;
                                d["comm_small_tiles"] = pl.comm_small_tiles;
+                               d["pivot"] = pl.pivot;
                                d["bcast"] = e.eng->bcast_algo();
                                d["bcast_tuning"] = e.comm->bcast_report();
                                d["comm"] = e.comm->describe();
@@ -534,6 +544,7 @@ PYBIND11_MODULE(_C, mod) {
     if (d.contains("eps")) c.solve.eps = d["eps"].cast<double>();
     if (d.contains("sync_debug")) c.solve.sync_debug = d["sync_debug"].cast<bool>();
     if (d.contains("depth")) c.solve.depth = d["depth"].cast<int>();
+    if (d.contains("pivot")) c.solve.pivot = parse_pivot(d["pivot"].cast<std::string>());
     if (d.contains("profile")) c.solve.profile = d["profile"].cast<bool>();
     if (d.contains("rhs")) c.rhs = d["rhs"].cast<std::string>();
     if (d.contains("keep_solution")) c.keep_solution = d["keep_solution"].cast<bool>();

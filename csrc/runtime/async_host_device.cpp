@@ -240,6 +240,18 @@ void AsyncHostDevice::block_inverse(DType dt, const void* Lt, int64_t ldl, void*
                                     double thresh, int s) {
   enqueue(s, [=] { inner_.block_inverse(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, s); });
 }
+void AsyncHostDevice::candidate_maxabs(DType dt, const void* Lt, int64_t ldl, double* scores, int32_t* valid,
+                                       const int32_t* used, const Layout& L, double thresh, int s) {
+  enqueue(s, [=] { inner_.candidate_maxabs(dt, Lt, ldl, scores, valid, used, L, thresh, s); });
+}
+void AsyncHostDevice::gather_candidate(DType dt, void* sel, const void* Lt, int64_t ldl, const PivotRec* rec,
+                                       const Layout& L, int s) {
+  enqueue(s, [=] { inner_.gather_candidate(dt, sel, Lt, ldl, rec, L, s); });
+}
+void AsyncHostDevice::commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1,
+                                       PivotRec* rec, const Layout& L, int s) {
+  enqueue(s, [=] { inner_.commit_candidate(dt, inv_t, inv1, valid1, rec, L, s); });
+}
 void AsyncHostDevice::pivot_local(const double* scores, const int32_t* valid, const int32_t* used,
                                   const int32_t* pos, const Layout& L, PivotRec* out, int s) {
   enqueue(s, [=] { inner_.pivot_local(scores, valid, used, pos, L, out, s); });

@@ -252,6 +252,21 @@ void HipDevice::block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t
   kern::block_inverse(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, hs(streams_[s]), sc, isc, variant);
   check_launch();
 }
+void HipDevice::candidate_maxabs(DType dt, const void* Lt, int64_t ldl, double* scores, int32_t* valid,
+                                 const int32_t* used, const Layout& L, double thresh, int s) {
+  kern::candidate_maxabs(dt, Lt, ldl, scores, valid, used, L, thresh, hs(streams_[s]));
+  check_launch();
+}
+void HipDevice::gather_candidate(DType dt, void* sel, const void* Lt, int64_t ldl, const PivotRec* rec,
+                                 const Layout& L, int s) {
+  kern::gather_candidate(dt, sel, Lt, ldl, rec, L, hs(streams_[s]));
+  check_launch();
+}
+void HipDevice::commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1, PivotRec* rec,
+                                 const Layout& L, int s) {
+  kern::commit_candidate(dt, inv_t, inv1, valid1, rec, L, hs(streams_[s]));
+  check_launch();
+}
 void HipDevice::pivot_local(const double* scores, const int32_t* valid, const int32_t* used,
                             const int32_t* pos, const Layout& L, PivotRec* out, int s) {
   kern::pivot_local(scores, valid, used, pos, L, out, hs(streams_[s]));

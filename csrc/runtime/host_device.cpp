@@ -241,6 +241,52 @@ void HostDevice::block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_
   });
 }
 
+void HostDevice::candidate_maxabs(DType dt, const void* Lt, int64_t ldl, double* scores, int32_t* valid,
+                                  const int32_t* used, const Layout& L, double thresh, int) {
+  const int64_t m = L.m;
+  for (int64_t b = 0; b < L.nblk; ++b) {
+    if (used[L.global_block(b)]) {
+      valid[b] = 0;
+      scores[b] = 0;
+      continue;
+    }
+    double mx = 0.0;
+    for (int64_t c = 0; c < m; ++c)
+      for (int64_t i = 0; i < m; ++i) {
+        const int64_t idx = c * ldl + b * m + i;
+        const double v = dt == DType::F64 ? tp<double>(Lt)[idx] : (double)tp<float>(Lt)[idx];
+        mx = std::max(mx, std::fabs(v));
+      }
+    scores[b] = -mx;
+    valid[b] = (mx >= thresh && std::isfinite(mx)) ? 1 : 0;
+  }
+}
+
+void HostDevice::gather_candidate(DType dt, void* sel, const void* Lt, int64_t ldl, const PivotRec* rec,
+                                  const Layout& L, int) {
+  const int64_t m = L.m;
+  const bool ok = rec->valid != 0;
+  const int64_t b = ok ? rec->phys / L.p : 0;
+  for (int64_t c = 0; c < m; ++c)
+    for (int64_t i = 0; i < m; ++i) {
+      const int64_t src = c * ldl + b * m + i, dst = c * m + i;
+      if (dt == DType::F64)
+        tp<double>(sel)[dst] = ok ? tp<double>(Lt)[src] : (c == i ? -1.0 : 0.0);
+      else
+        tp<float>(sel)[dst] = ok ? tp<float>(Lt)[src] : (c == i ? -1.0f : 0.0f);
+    }
+}
+
+void HostDevice::commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1, PivotRec* rec,
+                                  const Layout& L, int) {
+  if (!rec->valid || !valid1[0]) {
+    rec->valid = 0;
+    return;
+  }
+  const size_t blk = (size_t)L.m * L.m * dtype_size(dt);
+  std::memcpy(static_cast<char*>(inv_t) + (size_t)(rec->phys / L.p) * blk, inv1, blk);
+}
+
 void HostDevice::pivot_local(const double* scores, const int32_t* valid, const int32_t* used,
                              const int32_t* pos, const Layout& L, PivotRec* out, int) {
   PivotRec best = pivot_invalid();

@@ -187,6 +187,7 @@ Engine::Policy Engine::policy() const {
   p.reserve_cus = reserved_cus_;
   p.block_inverse = dev_.on_gpu() ? kern::block_inverse_kernel_name(opt_.dtype, L_.m, bi_hint_) : "host";
   p.comm_small_tiles = comm_small_tiles_;
+  p.pivot = opt_.pivot == PivotRule::Partial ? "partial" : "block-min-inv-norm";
   return p;
 }
 
@@ -255,6 +256,16 @@ void Engine::alloc_work(int64_t wmax) {
   T_ = dev_.alloc((size_t)m * wmax * es);
   RP_ = dev_.alloc((size_t)m * dm * es);
   inv_ = dev_.alloc((size_t)std::max<int64_t>(L_.nblk, 1) * m * m * es);
+  if (opt_.pivot == PivotRule::Partial) {
+    L1_ = Layout::make(m, m, 1, 0);
+    sel_ = dev_.alloc((size_t)m * m * es);
+    inv1_ = dev_.alloc((size_t)m * m * es);
+    score1_ = static_cast<double*>(dev_.alloc(sizeof(double)));
+    valid1_ = static_cast<int32_t*>(dev_.alloc(sizeof(int32_t)));
+    used1_ = static_cast<int32_t*>(dev_.alloc(sizeof(int32_t)));
+    dev_.memset0(used1_, sizeof(int32_t), S_SIDE);
+    dev_.sync_stream(S_SIDE);
+  }
   // the candidate-inverse kernel's scratch, now: not lazily inside the first timed pivot search
   dev_.prepare_block_inverse(opt_.dtype, L_, bi_hint_);
   scores_ = static_cast<double*>(dev_.alloc(sizeof(double) * std::max<int64_t>(L_.nblk, 1)));
@@ -286,7 +297,9 @@ void Engine::alloc_work(int64_t wmax) {
 }
 
 void Engine::free_work() {
-  std::vector<void**> dptrs = {&T_, &RP_, &inv_, reinterpret_cast<void**>(&scores_),
+  std::vector<void**> dptrs = {&T_, &RP_, &inv_, &sel_, &inv1_, reinterpret_cast<void**>(&score1_),
+                               reinterpret_cast<void**>(&valid1_), reinterpret_cast<void**>(&used1_),
+                               reinterpret_cast<void**>(&scores_),
                                reinterpret_cast<void**>(&valid_), reinterpret_cast<void**>(&pos_),
                                reinterpret_cast<void**>(&phys_at_), reinterpret_cast<void**>(&used_),
                                reinterpret_cast<void**>(&seq_), reinterpret_cast<void**>(&myrec_),
@@ -479,37 +492,51 @@ double Engine::norm_inf() {
 }
 
 // ---------------------------------------------------------------- pivot search (SIDE stream)
-void Engine::select(int64_t t, const void* Lt) {
+void Engine::select(int64_t t, const void* Lt, bool full) {
   const int par = (int)(t & 1);
   const double thresh = opt_.eps * norm_a_;
   Range rg(opt_.profile, "gj:select");
   int pe = prof_begin(S_SIDE);
-  if (L_.nblk > 0) {
-    dev_.set_block_inverse_hint(bi_hint_);  // per call: a device may be shared with other users
-    dev_.block_inverse(opt_.dtype, Lt, L_.rows, inv_, scores_, valid_, used_, L_, thresh, S_SIDE);
+  if (opt_.pivot == PivotRule::Partial && !full) {
+    // largest-magnitude local candidate, then its block alone inverted (record cleared if singular)
+    if (L_.nblk > 0) dev_.candidate_maxabs(opt_.dtype, Lt, L_.rows, scores_, valid_, used_, L_, thresh, S_SIDE);
+    dev_.pivot_local(scores_, valid_, used_, pos_, L_, myrec_, S_SIDE);
+    dev_.gather_candidate(opt_.dtype, sel_, Lt, L_.rows, myrec_, L_, S_SIDE);
+    dev_.set_block_inverse_hint(bi_hint_);
+    dev_.block_inverse(opt_.dtype, sel_, L_.m, inv1_, score1_, valid1_, used1_, L1_, thresh, S_SIDE);
     dev_.set_block_inverse_hint(-1);
-  }
-  if (L_.p == 1) {
-    // one rank: the local record is the gathered set -> local argmin + book-keeping in one launch;
-    // the result goes straight to pinned host memory (no copy kernel), the host polls its step field
-    piv_host_[par].step = -1;
-    dev_.pivot_select_single(scores_, valid_, L_, (int32_t)t, pos_, phys_at_, used_, seq_, myrec_,
-                             piv_dev_, &piv_host_[par], S_SIDE);
+    dev_.commit_candidate(opt_.dtype, inv_, inv1_, valid1_, myrec_, L_, S_SIDE);
     prof_end(PH_PIVOT, pe, S_SIDE);
   } else {
-    dev_.pivot_local(scores_, valid_, used_, pos_, L_, myrec_, S_SIDE);
-    prof_end(PH_PIVOT, pe, S_SIDE);
-    if (hang_step_ == t) {  // GJ_TEST_HANG: this rank never joins the exchange of step t
+    if (L_.nblk > 0) {
+      dev_.set_block_inverse_hint(bi_hint_);  // per call: a device may be shared with other users
+      dev_.block_inverse(opt_.dtype, Lt, L_.rows, inv_, scores_, valid_, used_, L_, thresh, S_SIDE);
+      dev_.set_block_inverse_hint(-1);
+    }
+    if (L_.p == 1) {
+      // one rank: the local record is the gathered set -> local argmin + book-keeping in one launch;
+      // the result goes straight to pinned host memory (no copy kernel), the host polls its step field
       piv_host_[par].step = -1;
+      dev_.pivot_select_single(scores_, valid_, L_, (int32_t)t, pos_, phys_at_, used_, seq_, myrec_,
+                               piv_dev_, &piv_host_[par], S_SIDE);
+      prof_end(PH_PIVOT, pe, S_SIDE);
+      dev_.record(ev_sel_[par], S_SIDE);
+      dbg_sync();
       return;
     }
-    pe = prof_begin(S_SIDE);
-    comm_.allgather(dev_, myrec_, recs_, sizeof(PivotRec), S_SIDE);
-    piv_host_[par].step = -1;
-    dev_.pivot_global(recs_, (int32_t)L_.p, (int32_t)t, pos_, phys_at_, used_, seq_, piv_dev_,
-                      &piv_host_[par], S_SIDE);
-    prof_end(PH_EXCHANGE, pe, S_SIDE);
+    dev_.pivot_local(scores_, valid_, used_, pos_, L_, myrec_, S_SIDE);
+    prof_end(PH_PIVOT, pe, S_SIDE);
   }
+  if (hang_step_ == t) {  // GJ_TEST_HANG: this rank never joins the exchange of step t
+    piv_host_[par].step = -1;
+    return;
+  }
+  pe = prof_begin(S_SIDE);
+  if (L_.p > 1) comm_.allgather(dev_, myrec_, recs_, sizeof(PivotRec), S_SIDE);
+  piv_host_[par].step = -1;
+  dev_.pivot_global(L_.p > 1 ? recs_ : myrec_, (int32_t)L_.p, (int32_t)t, pos_, phys_at_, used_, seq_, piv_dev_,
+                    &piv_host_[par], S_SIDE);
+  prof_end(PH_EXCHANGE, pe, S_SIDE);
   dev_.record(ev_sel_[par], S_SIDE);
   dbg_sync();
 }
@@ -553,7 +580,14 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
     }
     select(t, Lt);
     wait_pivot((int)(t & 1), t, host_wait);
-    const PivotResult r = piv_host_[t & 1];
+    PivotResult r = piv_host_[t & 1];
+    if (!r.found && opt_.pivot == PivotRule::Partial) {
+      // every rank's largest-magnitude candidate was singular: this step takes the full search
+      st.pivot_fallbacks++;
+      select(t, Lt, /*full=*/true);
+      wait_pivot((int)(t & 1), t, host_wait);
+      r = piv_host_[t & 1];
+    }
     if (!r.found) {
       comm_.drain_all(dev_);
       st.status = Status::Singular;

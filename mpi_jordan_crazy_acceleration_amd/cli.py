@@ -56,6 +56,7 @@ def main(argv=None) -> int:
     ap.add_argument("--print-max", type=int, default=10)
     ap.add_argument("--eps", type=float, default=1e-15)
     ap.add_argument("--depth", type=int, default=0)
+    ap.add_argument("--pivot", choices=["block-min-inv-norm", "partial"], default="block-min-inv-norm")
     ap.add_argument("--chunk-cols", type=int, default=0)
     ap.add_argument("--host-threads", type=int, default=0)
     ap.add_argument("--comm-timeout", type=float, default=600.0)
@@ -100,7 +101,7 @@ def main(argv=None) -> int:
     try:
         try:
             solver = DistributedGaussJordan(n, m, dtype=args.dtype, chunk_cols=args.chunk_cols, eps=args.eps,
-                                            host_threads=args.host_threads, depth=args.depth,
+                                            host_threads=args.host_threads, depth=args.depth, pivot=args.pivot,
                                             local_rank=local if gpu else None)
         except C.GJError as e:  # agreed on every rank inside the constructor
             out("Not enough memory!\n" if e.status == 2 else f"error: {e}\n")

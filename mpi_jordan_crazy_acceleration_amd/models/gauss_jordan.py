@@ -43,7 +43,8 @@ class GaussJordan:
     comm: str = "auto"  # auto | rccl | loopback | async (stream-ordered virtual ranks)
     jitter_us: float = 0.0  # comm="async": random per-rank arrival delays (race screening)
     chunk_cols: int = 0
-    depth: int = 0  # 0 = auto (2 up to N=8192, else 4)
+    depth: int = 0  # 0 = auto (engine.hpp)
+    pivot: str = "block-min-inv-norm"  # or "partial" (block partial pivoting, SolveOptions::pivot)
     eps: float = 1e-15
     sync_debug: bool = False
     residual: str = "always"
@@ -54,6 +55,7 @@ class GaussJordan:
         dev = _default_device() if self.device == "auto" else self.device
         cfg = dict(n=int(n), m=int(self.block_size), ranks=int(self.ranks), device=dev,
                    dtype=self.dtype, comm=self.comm, chunk_cols=int(self.chunk_cols), depth=int(self.depth),
+                   pivot=self.pivot,
                    eps=float(self.eps),
                    sync_debug=bool(self.sync_debug), residual=self.residual,
                    host_threads=int(self.host_threads), jitter_us=float(self.jitter_us))
@@ -109,7 +111,8 @@ class GaussJordan:
         n = a.shape[0]
         idx = a.device.index if a.device.index is not None else torch.cuda.current_device()
         eng = C.Engine(_hip_device(idx), C.self_comm(), n, int(self.block_size), self.dtype,
-                       int(self.chunk_cols), float(self.eps), bool(self.sync_debug), int(self.depth))
+                       int(self.chunk_cols), float(self.eps), bool(self.sync_debug), int(self.depth),
+                       pivot=self.pivot)
         torch.cuda.synchronize(a.device)  # A may have been written on torch's stream
         eng.upload_rows_device(a.data_ptr(), a.stride(0))
         st = eng.solve()
