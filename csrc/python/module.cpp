@@ -343,6 +343,15 @@ PYBIND11_MODULE(_C, mod) {
     GJ_REQUIRE(sc != nullptr, "shadow_reset: not a shadow communicator");
     sc->reset();
   });
+  // One broadcast of `bytes` from `root` through a shadow communicator on the host (cost accounting
+  // only: tests of the per-link model).
+  mod.def("shadow_bcast_probe", [](std::shared_ptr<Comm> c, size_t bytes, int root) {
+    auto* sc = dynamic_cast<ShadowComm*>(c.get());
+    GJ_REQUIRE(sc != nullptr, "shadow_bcast_probe: not a shadow communicator");
+    HostDevice dev(1);
+    std::vector<char> buf(bytes);
+    sc->bcast(dev, buf.data(), bytes, root, S_COMM);
+  });
   mod.def("shadow_modelled_us", [](std::shared_ptr<Comm> c) {
     auto* sc = dynamic_cast<ShadowComm*>(c.get());
     GJ_REQUIRE(sc != nullptr, "shadow_modelled_us: not a shadow communicator");
