@@ -235,6 +235,10 @@ class Engine {
   void* At_[3] = {nullptr, nullptr, nullptr};
   void* Rb_[2] = {nullptr, nullptr};   // stacked normalised pivot rows, chunk-major (d*m) x npad
   void* PP_[2] = {nullptr, nullptr};   // panel pieces: R_t restricted to the panel's columns, (d*m) x (d*m)
+  // look-ahead rows: a panel's normalised pivot rows restricted to the NEXT panel's block columns,
+  // (q*m) x (qn*m), step-major; formed and broadcast ahead of the first chunk so that the next
+  // panel's look-ahead update (and with it the next pivot chain) does not wait for a whole chunk
+  void* LA_[2] = {nullptr, nullptr};
   void* Lrow_[2][kMaxDepth] = {};      // multipliers of pivot row s_t for earlier panel steps, K-major
   void* Ht_[2][kMaxDepth] = {};        // H_t^T
   void* T_ = nullptr;                  // row-update temp, m x Wmax
@@ -269,6 +273,7 @@ class Engine {
   // events
   int ev_L_ = -1, ev_main_ = -1, ev_sel_[2] = {-1, -1}, ev_edit_[2] = {-1, -1};
   int ev_pp_[2][kMaxDepth] = {};
+  int ev_la_[2] = {-1, -1};            // LA_[par] formed and broadcast (COMM)
   std::vector<int> ev_c_;        // per chunk: MAIN finished the panel update of that chunk
   std::vector<int> ev_b_[2];     // per chunk: all stacked rows of that chunk broadcast
   std::vector<int> pev_pool_;    // profiling events (timing enabled), reused across solves

@@ -205,7 +205,7 @@ int Engine::alloc_buffers(std::string& why) {
   int64_t wmax = 0;
   for (size_t c = 0; c < cb0_.size(); ++c) wmax = std::max(wmax, chunk_w((int64_t)c));
   const size_t need_matrix = 2 * panel;
-  const size_t need_work = 3 * (size_t)dm * rows * es + 2 * (size_t)dm * npad * es +
+  const size_t need_work = 3 * (size_t)dm * rows * es + 2 * (size_t)dm * npad * es + 4 * (size_t)dm * dm * es +
                            (size_t)std::max<int64_t>(L_.nblk, 1) * m * m * es + (size_t)m * wmax * es +
                            dev_.block_inverse_scratch_bytes(opt_.dtype, L_, bi_hint_);
   const size_t avail = dev_.on_gpu() ? dev_.free_memory() : SIZE_MAX;
@@ -248,6 +248,7 @@ void Engine::alloc_work(int64_t wmax) {
   for (int i = 0; i < 2; ++i) {
     Rb_[i] = dev_.alloc((size_t)dm * npad * es);
     PP_[i] = dev_.alloc((size_t)dm * dm * es);
+    LA_[i] = dev_.alloc((size_t)dm * dm * es);
     for (int j = 0; j < d_; ++j) {
       Lrow_[i][j] = dev_.alloc((size_t)std::max<int64_t>(j, 1) * m * m * es);
       Ht_[i][j] = dev_.alloc((size_t)m * m * es);
@@ -291,6 +292,7 @@ void Engine::alloc_work(int64_t wmax) {
     ev_sel_[i] = dev_.create_event();
     ev_edit_[i] = dev_.create_event();
     for (int j = 0; j < kMaxDepth; ++j) ev_pp_[i][j] = dev_.create_event();
+    ev_la_[i] = dev_.create_event();
     for (size_t c = 0; c < cb0_.size(); ++c) ev_b_[i].push_back(dev_.create_event());
   }
   for (size_t c = 0; c < cb0_.size(); ++c) ev_c_.push_back(dev_.create_event());
@@ -309,6 +311,7 @@ void Engine::free_work() {
   for (int i = 0; i < 2; ++i) {
     dptrs.push_back(&Rb_[i]);
     dptrs.push_back(&PP_[i]);
+    dptrs.push_back(&LA_[i]);
     for (int j = 0; j < kMaxDepth; ++j) {
       dptrs.push_back(&Lrow_[i][j]);
       dptrs.push_back(&Ht_[i][j]);
@@ -676,6 +679,52 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
   const int64_t pc0 = t0 * m, pc1 = (t0 + q) * m;  // panel columns
   dev_.wait(S_COMM, ev_pp_[par][q - 1]);  // all panel pieces, multiplier rows and H_t (SIDE)
   cur_phase_ = "pivot-row broadcast";
+  static const bool no_la = std::getenv("GJ_NO_LA") && std::atoi(std::getenv("GJ_NO_LA")) > 0;  // A/B (temporary)
+  if (has_next && !no_la) {
+    // The next panel's block columns first, on their own (LA_[par], step-major, ld wla): MAIN's
+    // look-ahead update of panel v+1 needs only these, so the next pivot chain starts after a
+    // (q*m) x (qn*m) broadcast instead of after a whole chunk's.  The chunk pass below broadcasts
+    // these columns again with the rest of their chunk (MAIN's chunk update skips them).
+    const int64_t xa = panel_t0(v + 1) * m, wla = panel_q(v + 1) * m;
+    if (wait_main) dev_.wait(S_COMM, ev_c_[chunk_of_[panel_t0(v + 1)]]);
+    std::vector<BcastOp> lops;
+    auto lflush = [&]() {
+      if (lops.empty()) return;
+      const int pb = prof_begin(S_COMM);
+      comm_.bcast_many(dev_, lops, S_COMM);
+      prof_end(PH_BCAST, pb, S_COMM);
+      lops.clear();
+    };
+    GemmExtra lat;
+    lat.latency = true;
+    for (int64_t j = 0; j < q; ++j) {
+      const PivotResult& r = piv_[par][j];
+      char* seg = elem(LA_[par], j * m * wla);
+      for (const auto& o : lops)  // R_j needs the earlier steps' rows (see the chunk pass)
+        if (o.root != r.owner) {
+          lflush();
+          break;
+        }
+      if (r.owner == L_.k) {
+        const int pe = prof_begin(S_COMM);
+        const int64_t sl = r.phys / L_.p;
+        if (j == 0) {
+          dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, wla, m, Ht_[par][j], m,
+                    elem(X_, sl * m * npad + xa), npad, seg, wla, S_COMM, lat);
+        } else {
+          dev_.copy2d(T_, wla * es, elem(X_, sl * m * npad + xa), npad * es, wla * es, m, S_COMM);
+          dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, m, wla, j * m, Lrow_[par][j], m, LA_[par], wla,
+                    T_, wla, S_COMM, lat);
+          dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, wla, m, Ht_[par][j], m, T_, wla, seg, wla,
+                    S_COMM, lat);
+        }
+        prof_end(PH_NORMALISE, pe, S_COMM);
+      }
+      lops.push_back(BcastOp{seg, (size_t)m * wla * es, (int)r.owner});
+    }
+    lflush();
+    dev_.record(ev_la_[par], S_COMM);
+  }
   for (int64_t i = 0; i < C; ++i) {
     const int64_t c = (start + i) % C;
     const int64_t c0 = cb0_[c] * m, c1 = cb1_[c] * m, W = c1 - c0;
@@ -763,12 +812,17 @@ void Engine::big_update(int64_t u) {
     const int ms = S_MAIN;
     x0 = tn * m;
     x1 = (tn + qn) * m;
-    dev_.wait(ms, ev_b_[par][cn]);
+    static const bool no_la = std::getenv("GJ_NO_LA") && std::atoi(std::getenv("GJ_NO_LA")) > 0;  // A/B (temporary)
+    dev_.wait(ms, no_la ? ev_b_[par][cn] : ev_la_[par]);  // the look-ahead rows of panel u (chunk_pipeline)
     const int pe = prof_begin(ms);
     if (rows > 0) {
-      dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, x1 - x0, K, At, rows,
-                rb_chunk(par, cn) + (x0 - cb0_[cn] * m) * (int64_t)esz(), chunk_w(cn), elem(X_, x0),
-                npad, ms, prows);
+      if (no_la)
+        dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, x1 - x0, K, At, rows,
+                  rb_chunk(par, cn) + (x0 - cb0_[cn] * m) * (int64_t)esz(), chunk_w(cn), elem(X_, x0),
+                  npad, ms, prows);
+      else
+        dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, x1 - x0, K, At, rows, LA_[par], x1 - x0,
+                  elem(X_, x0), npad, ms, prows);
       dev_.extract_neg_t(opt_.dtype, At_next, rows, X_, npad, rows, x0, m, ms);
     }
     prof_end(PH_UPDATE, pe, ms);
