@@ -679,8 +679,7 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
   const int64_t pc0 = t0 * m, pc1 = (t0 + q) * m;  // panel columns
   dev_.wait(S_COMM, ev_pp_[par][q - 1]);  // all panel pieces, multiplier rows and H_t (SIDE)
   cur_phase_ = "pivot-row broadcast";
-  static const bool no_la = std::getenv("GJ_NO_LA") && std::atoi(std::getenv("GJ_NO_LA")) > 0;  // A/B (temporary)
-  if (has_next && !no_la) {
+  if (has_next) {
     // The next panel's block columns first, on their own (LA_[par], step-major, ld wla): MAIN's
     // look-ahead update of panel v+1 needs only these, so the next pivot chain starts after a
     // (q*m) x (qn*m) broadcast instead of after a whole chunk's.  The chunk pass below broadcasts
@@ -812,17 +811,15 @@ void Engine::big_update(int64_t u) {
     const int ms = S_MAIN;
     x0 = tn * m;
     x1 = (tn + qn) * m;
-    static const bool no_la = std::getenv("GJ_NO_LA") && std::atoi(std::getenv("GJ_NO_LA")) > 0;  // A/B (temporary)
-    dev_.wait(ms, no_la ? ev_b_[par][cn] : ev_la_[par]);  // the look-ahead rows of panel u (chunk_pipeline)
+    (void)cn;
+    // the look-ahead rows of panel u (chunk_pipeline): N = 16384 emulated p = 4 / 8 at 50 GB/s per
+    // link 0.0669 -> 0.0595 s / 0.0485 -> 0.0431 s against waiting for the whole first chunk
+    // (profiles/emu_direct_r3.md)
+    dev_.wait(ms, ev_la_[par]);
     const int pe = prof_begin(ms);
     if (rows > 0) {
-      if (no_la)
-        dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, x1 - x0, K, At, rows,
-                  rb_chunk(par, cn) + (x0 - cb0_[cn] * m) * (int64_t)esz(), chunk_w(cn), elem(X_, x0),
-                  npad, ms, prows);
-      else
-        dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, x1 - x0, K, At, rows, LA_[par], x1 - x0,
-                  elem(X_, x0), npad, ms, prows);
+      dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, x1 - x0, K, At, rows, LA_[par], x1 - x0,
+                elem(X_, x0), npad, ms, prows);
       dev_.extract_neg_t(opt_.dtype, At_next, rows, X_, npad, rows, x0, m, ms);
     }
     prof_end(PH_UPDATE, pe, ms);
