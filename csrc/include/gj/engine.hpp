@@ -239,6 +239,7 @@ class Engine {
   // (q*m) x (qn*m), step-major; formed and broadcast ahead of the first chunk so that the next
   // panel's look-ahead update (and with it the next pivot chain) does not wait for a whole chunk
   void* LA_[2] = {nullptr, nullptr};
+  void* T2_ = nullptr;                 // LA temp when LA runs on SIDE, m x (d*m)
   void* Lrow_[2][kMaxDepth] = {};      // multipliers of pivot row s_t for earlier panel steps, K-major
   void* Ht_[2][kMaxDepth] = {};        // H_t^T
   void* T_ = nullptr;                  // row-update temp, m x Wmax

@@ -206,6 +206,7 @@ int Engine::alloc_buffers(std::string& why) {
   for (size_t c = 0; c < cb0_.size(); ++c) wmax = std::max(wmax, chunk_w((int64_t)c));
   const size_t need_matrix = 2 * panel;
   const size_t need_work = 3 * (size_t)dm * rows * es + 2 * (size_t)dm * npad * es + 4 * (size_t)dm * dm * es +
+                           (size_t)m * dm * es +
                            (size_t)std::max<int64_t>(L_.nblk, 1) * m * m * es + (size_t)m * wmax * es +
                            dev_.block_inverse_scratch_bytes(opt_.dtype, L_, bi_hint_);
   const size_t avail = dev_.on_gpu() ? dev_.free_memory() : SIZE_MAX;
@@ -256,6 +257,7 @@ void Engine::alloc_work(int64_t wmax) {
   }
   T_ = dev_.alloc((size_t)m * wmax * es);
   RP_ = dev_.alloc((size_t)m * dm * es);
+  T2_ = dev_.alloc((size_t)m * dm * es);
   inv_ = dev_.alloc((size_t)std::max<int64_t>(L_.nblk, 1) * m * m * es);
   if (opt_.pivot == PivotRule::Partial) {
     L1_ = Layout::make(m, m, 1, 0);
@@ -299,7 +301,7 @@ void Engine::alloc_work(int64_t wmax) {
 }
 
 void Engine::free_work() {
-  std::vector<void**> dptrs = {&T_, &RP_, &inv_, &sel_, &inv1_, reinterpret_cast<void**>(&score1_),
+  std::vector<void**> dptrs = {&T_, &T2_, &RP_, &inv_, &sel_, &inv1_, reinterpret_cast<void**>(&score1_),
                                reinterpret_cast<void**>(&valid1_), reinterpret_cast<void**>(&used1_),
                                reinterpret_cast<void**>(&scores_),
                                reinterpret_cast<void**>(&valid_), reinterpret_cast<void**>(&pos_),
@@ -685,13 +687,19 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
     // (q*m) x (qn*m) broadcast instead of after a whole chunk's.  The chunk pass below broadcasts
     // these columns again with the rest of their chunk (MAIN's chunk update skips them).
     const int64_t xa = panel_t0(v + 1) * m, wla = panel_q(v + 1) * m;
-    if (wait_main) dev_.wait(S_COMM, ev_c_[chunk_of_[panel_t0(v + 1)]]);
+    // at p > 1 on SIDE, right behind the panel pieces, with SIDE's communicator: emulated N = 16384
+    // p = 4 at 50 GB/s per link 0.0588 -> 0.0564 s (80 % of the transfer hidden), p = 8 0.0430 ->
+    // 0.0425 s; one rank keeps it on COMM (N = 8192 28.66 vs 28.84 ms) -- profiles/emu_direct_r3.md
+    const bool la_side = L_.p > 1;
+    const int ls = la_side ? S_SIDE : S_COMM;
+    void* Tl = la_side ? T2_ : T_;
+    if (wait_main) dev_.wait(ls, ev_c_[chunk_of_[panel_t0(v + 1)]]);
     std::vector<BcastOp> lops;
     auto lflush = [&]() {
       if (lops.empty()) return;
-      const int pb = prof_begin(S_COMM);
-      comm_.bcast_many(dev_, lops, S_COMM);
-      prof_end(PH_BCAST, pb, S_COMM);
+      const int pb = prof_begin(ls);
+      comm_.bcast_many(dev_, lops, ls);
+      prof_end(PH_BCAST, pb, ls);
       lops.clear();
     };
     GemmExtra lat;
@@ -705,24 +713,24 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
           break;
         }
       if (r.owner == L_.k) {
-        const int pe = prof_begin(S_COMM);
+        const int pe = prof_begin(ls);
         const int64_t sl = r.phys / L_.p;
         if (j == 0) {
           dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, wla, m, Ht_[par][j], m,
-                    elem(X_, sl * m * npad + xa), npad, seg, wla, S_COMM, lat);
+                    elem(X_, sl * m * npad + xa), npad, seg, wla, ls, lat);
         } else {
-          dev_.copy2d(T_, wla * es, elem(X_, sl * m * npad + xa), npad * es, wla * es, m, S_COMM);
+          dev_.copy2d(Tl, wla * es, elem(X_, sl * m * npad + xa), npad * es, wla * es, m, ls);
           dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, m, wla, j * m, Lrow_[par][j], m, LA_[par], wla,
-                    T_, wla, S_COMM, lat);
-          dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, wla, m, Ht_[par][j], m, T_, wla, seg, wla,
-                    S_COMM, lat);
+                    Tl, wla, ls, lat);
+          dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, wla, m, Ht_[par][j], m, Tl, wla, seg, wla,
+                    ls, lat);
         }
-        prof_end(PH_NORMALISE, pe, S_COMM);
+        prof_end(PH_NORMALISE, pe, ls);
       }
       lops.push_back(BcastOp{seg, (size_t)m * wla * es, (int)r.owner});
     }
     lflush();
-    dev_.record(ev_la_[par], S_COMM);
+    dev_.record(ev_la_[par], ls);
   }
   for (int64_t i = 0; i < C; ++i) {
     const int64_t c = (start + i) % C;
