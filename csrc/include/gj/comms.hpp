@@ -178,6 +178,7 @@ struct CostModel {
 class ShadowComm : public Comm {
  public:
   explicit ShadowComm(int p, CostModel cm = CostModel()) : p_(p), cm_(cm) {}
+  ~ShadowComm() override;
   int size() const override { return p_; }
   int rank() const override { return 0; }
   std::string describe() const override;
@@ -201,7 +202,13 @@ class ShadowComm : public Comm {
   CostModel cm_;
   int64_t step_ = 0;
   double modelled_us_ = 0;
-  std::vector<char> host_;
+  // the synthetic peers' pivot records, staged in pinned memory: a ring of kSlots steps, so the
+  // record copy of step t never waits for the host (the engine's own wait for step t's pivot
+  // orders it before slot t is reused, kSlots steps later) -- a real all-gather has no host sync
+  static constexpr int kSlots = 8;
+  char* pin_ = nullptr;      // hipHostMalloc'd (GPU device) or malloc'd (host device)
+  bool pin_hip_ = false;
+  size_t pin_bytes_ = 0;
 };
 
 }  // namespace gj

@@ -1,5 +1,8 @@
 // ShadowComm: see gj/comms.hpp.
+#include <hip/hip_runtime.h>
+
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "gj/comms.hpp"
@@ -32,6 +35,12 @@ void ShadowComm::group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) {
   cost(dev, busiest, 1, s);
 }
 
+ShadowComm::~ShadowComm() {
+  if (!pin_) return;
+  if (pin_hip_) (void)hipHostFree(pin_);
+  else std::free(pin_);
+}
+
 void ShadowComm::allgather(Device& dev, const void* send, void* recv, size_t bytes, int s) {
   cost(dev, bytes * (p_ - 1), 1, s);
   dev.copy(recv, send, bytes, s);  // slot 0 = own contribution
@@ -40,8 +49,26 @@ void ShadowComm::allgather(Device& dev, const void* send, void* recv, size_t byt
     return;
   }
   const int64_t t = step_++;
-  host_.assign((size_t)p_ * bytes, 0);
-  auto* recs = reinterpret_cast<PivotRec*>(host_.data());
+  const size_t slot = (size_t)p_ * bytes;
+  if (!pin_ || pin_hip_ != dev.on_gpu() || pin_bytes_ < kSlots * slot) {
+    dev.sync_all();
+    if (pin_) {
+      if (pin_hip_) (void)hipHostFree(pin_);
+      else std::free(pin_);
+      pin_ = nullptr;
+    }
+    pin_hip_ = dev.on_gpu();
+    pin_bytes_ = kSlots * slot;
+    if (pin_hip_) {
+      void* p = nullptr;
+      if (hipHostMalloc(&p, pin_bytes_, hipHostMallocDefault) != hipSuccess)
+        throw Error(Status::NoMemory, "ShadowComm: pinned record ring");
+      pin_ = static_cast<char*>(p);
+    } else {
+      pin_ = static_cast<char*>(std::malloc(pin_bytes_));
+    }
+  }
+  auto* recs = reinterpret_cast<PivotRec*>(pin_ + (size_t)(t % kSlots) * slot);
   for (int q = 1; q < p_; ++q) recs[q] = pivot_invalid();
   const int q = (int)(t % p_);
   if (q != 0) {
@@ -50,8 +77,7 @@ void ShadowComm::allgather(Device& dev, const void* send, void* recv, size_t byt
     recs[q].phys = (int32_t)t;
     recs[q].valid = 1;
   }
-  dev.copy(static_cast<char*>(recv) + bytes, host_.data() + bytes, (p_ - 1) * bytes, s);
-  dev.sync_stream(s);  // host_ is reused by the next step
+  dev.copy(static_cast<char*>(recv) + bytes, reinterpret_cast<char*>(recs) + bytes, (p_ - 1) * bytes, s);
 }
 
 void ShadowComm::bcast(Device& dev, void* buf, size_t bytes, int root, int s) {
