@@ -12,6 +12,9 @@
   workgroups < 256 CUs.  README.md, "Progress of the two communicators".
 * ``HIP_FORCE_DEV_KERNARG=1``: kernel arguments in device memory (measured: =0 costs 3.4 % at
   N = 8192, profiles/small_n_sweep.md).
+* ``HSA_ENABLE_IPC_MODE_LEGACY=0`` unless set: RCCL's inter-process buffers between the rank
+  processes of one node go through dma-buf IPC (the legacy IPC handles are not supported by the
+  drivers this is deployed on: ``hipIpcGetMemHandle: invalid argument``).
 
 Values already set higher are kept; nothing is ever lowered or raised above 32.
 """
@@ -31,4 +34,5 @@ def configure_runtime_env(environ=None) -> dict:
     if cur < MIN_HW_QUEUES and env.get("GJ_KEEP_HW_QUEUES", "0") != "1":  # (A/B measurements only)
         env["GPU_MAX_HW_QUEUES"] = str(MIN_HW_QUEUES)
     env.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return {"GPU_MAX_HW_QUEUES": env["GPU_MAX_HW_QUEUES"], "HIP_FORCE_DEV_KERNARG": env["HIP_FORCE_DEV_KERNARG"]}
