@@ -109,9 +109,9 @@ class Device {
     (void)s; (void)nwg; (void)us; (void)lds_bytes;
   }
   // Keep the MAIN (trailing-update) stream off `n` CUs so the latency-critical SIDE/COMM kernels
-  // always find idle CUs (mode 0: CUs 0..n-1 of the mask, mode 1: spread over the mask).
+  // always find idle CUs (the first n bits of the CU mask; n = 32 is one CU per shader engine).
   // Returns the number of CUs actually reserved.  Call while the device is idle.
-  virtual int reserve_cus(int n, int mode) { (void)n; (void)mode; return 0; }
+  virtual int reserve_cus(int n) { (void)n; return 0; }
 
   // ---- kernels ----
   // X (layout.rows x npad, ld npad) := A' restricted to this rank's block rows.

@@ -58,7 +58,6 @@ struct SolveOptions {
   bool profile = false;     // per-phase device timers (HIP events) + roctx ranges
   double comm_timeout_s = 600;  // a host wait on a pivot longer than this is a peer failure
   int reserve_cus = -1;     // CUs kept free of the trailing update for the pivot path (-1 = auto)
-  int reserve_mode = 0;     // 0 = first CUs of the mask (measured best), 1 = spread
 };
 
 // Device time per phase (sum over the solve; phases on different streams overlap in time).

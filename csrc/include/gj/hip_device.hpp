@@ -33,10 +33,10 @@ class HipDevice : public Device {
   void sync_event(int ev) override;
   bool query_event(int ev) override;
  private:
-  int reserved_ = 0, reserve_mode_ = 0;
+  int reserved_ = 0;
 
  public:
-  int reserve_cus(int n, int mode) override;
+  int reserve_cus(int n) override;
   void sync_stream(int s) override;
   bool stream_idle(int s) override;
   void sync_all() override;

@@ -53,8 +53,8 @@ HipDevice::~HipDevice() {
 
 void HipDevice::activate() const { (void)hipSetDevice(dev_); }
 
-int HipDevice::reserve_cus(int n, int mode) {
-  if (n == reserved_ && mode == reserve_mode_) return reserved_;
+int HipDevice::reserve_cus(int n) {
+  if (n == reserved_) return reserved_;
   activate();
   hipDeviceProp_t prop;
   HIP_OK(hipGetDeviceProperties(&prop, dev_));
@@ -71,17 +71,14 @@ int HipDevice::reserve_cus(int n, int mode) {
     } else {
       std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
       for (int c = 0; c < ncu; ++c) mask[c / 32] |= 1u << (c % 32);
-      const int stride = std::max(1, ncu / n);
-      for (int i = 0; i < n; ++i) {
-        const int c = (mode == 0) ? i : i * stride;
-        mask[c / 32] &= ~(1u << (c % 32));
-      }
+      // the first n bits: bit i is a CU of XCC i % 8, shader engine (i / 8) % 4, so n = 32 takes
+      // one CU from every shader engine (bench/cu_mask_probe.hip, profiles/cu_reserve_sweep.md)
+      for (int i = 0; i < n; ++i) mask[i / 32] &= ~(1u << (i % 32));
       HIP_OK(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
     }
     streams_[role] = st;
   }
   reserved_ = n;
-  reserve_mode_ = mode;
   return n;
 }
 

@@ -114,13 +114,16 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   if (const char* e = std::getenv("GJ_RESERVE_CUS")) rc = std::atoi(e);
   // auto: up to N = 16384 the pivot chain is the critical path and its block inverses only start
   // on a CU no trailing-update workgroup occupies, so keep 32 CUs (1/8 of the chip) off the MAIN
-  // streams: N=8192 p=1 -12 %, emulated p=2/4/8 at N=16384 -10/-16/-14 %.  At N=32768 the GEMM is
-  // the critical path and the mask costs 4-10 % (profiles/cu_reserve_sweep.md) -- except on ranks
+  // stream -- the first 32 mask bits, i.e. one CU of every shader engine (bits interleave XCCs, then
+  // SEs: bench/cu_mask_probe.hip), since a launch's workgroups are split evenly over the 32 SEs and
+  // an unbalanced mask makes the smallest SE the straggler (profiles/cu_reserve_sweep.md):
+  // N=8192 p=1 -12 %, emulated p=2/4/8 at N=16384 -10/-16/-14 %.  At N=32768 the GEMM is the
+  // critical path and the mask costs 4-10 % (profiles/cu_reserve_sweep.md) -- except on ranks
   // with <= 4096 rows (p = 8 at N = 32768), where the pivot chain and the RCCL workgroups of its
   // collectives need the free CUs: under the communication-cost model p = 8 is 6.6 % faster with
   // the reservation at 100 GB/s, p = 2 / 4 are 9 / 6 % slower (profiles/cu_reserve_pgt1.md).
   if (rc < 0) rc = (dev_.on_gpu() && (L_.npad <= 16384 || small_rank)) ? 32 : 0;
-  reserved_cus_ = dev_.reserve_cus(rc, opt_.reserve_mode);
+  reserved_cus_ = dev_.reserve_cus(rc);
   // Candidate inverses on ranks whose trailing update holds every CU (p > 1 without a reservation:
   // the 16384- and 8192-row ranks of N = 32768) take the co-resident 4-wave form, which starts in
   // the slot one retiring trailing-update workgroup frees instead of waiting for a whole CU: the
