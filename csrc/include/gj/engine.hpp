@@ -179,8 +179,11 @@ class Engine {
   void select(int64_t t, const void* Lt, bool full = false);
   // Panel factorisation (pivot searches of its q steps, panel pieces, then the chunk pipeline of
   // the normalised pivot rows).  Returns false when the matrix is singular.
-  bool factor_panel(int64_t v, bool wait_main, SolveStats& st, double& host_wait);
+  void begin_panel(int64_t v);
+  bool factor_panel(int64_t v, SolveStats& st, double& host_wait);
+  void lookahead_rows(int64_t v, bool wait_main);
   void chunk_pipeline(int64_t v, bool wait_main);
+  void lookahead_update(int64_t u);
   void big_update(int64_t u);
   void finalize(const std::vector<int32_t>& seq);
   SolveStats solve_steps();

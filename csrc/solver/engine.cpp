@@ -557,11 +557,20 @@ GemmExtra Engine::pivot_rows_extra(int par, int64_t nsteps) const {
   return ex;
 }
 
-// Pivot searches of panel v.  Column t0 is ready (extracted into At[par] segment 0, event ev_L_);
-// every later column of the panel is brought up to date on the SIDE stream from the broadcast
-// panel pieces.  For every step: owner edits (Lrow save, H, multiplier rows -> [0..I]), then the
-// panel piece PP_t = H_t X^(t)[s_t, panel columns] on COMM and its (small) broadcast.
-bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& host_wait) {
+// The pivot search of panel v's first step, enqueued on SIDE behind MAIN's look-ahead (event
+// ev_L_: column t0 extracted into At[v % 3] segment 0).
+void Engine::begin_panel(int64_t v) {
+  cur_step_ = panel_t0(v);
+  cur_phase_ = "pivot search";
+  dev_.wait(S_SIDE, ev_L_);
+  select(panel_t0(v), At_[v % 3]);
+}
+
+// Pivot searches of panel v (the first one already enqueued by begin_panel); every later column
+// of the panel is brought up to date on the SIDE stream from the broadcast panel pieces.  For
+// every step: owner edits (Lrow save, H, multiplier rows -> [0..I]), then the panel piece
+// PP_t = H_t X^(t)[s_t, panel columns] and its (small) broadcast.
+bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
   const int par = (int)(v & 1);
   const int64_t m = L_.m, rows = L_.rows, npad = L_.npad, dm = (int64_t)d_ * m;
   const int64_t t0 = panel_t0(v), q = panel_q(v);
@@ -571,9 +580,7 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
     cur_step_ = t;
     cur_phase_ = "pivot search";
     void* Lt = elem(At_[v % 3], j * m * rows);
-    if (j == 0) {
-      dev_.wait(S_SIDE, ev_L_);
-    } else {
+    if (j > 0) {
       // column t after panel v-1 (look-ahead) and steps t0..t-1 of this panel
       dev_.wait(S_SIDE, ev_pp_[par][j - 1]);
       const int pe = prof_begin(S_SIDE);
@@ -585,8 +592,8 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
         dev_.extract_neg_t(opt_.dtype, Lt, rows, X_, npad, rows, t * m, m, S_SIDE);
       }
       prof_end(PH_COLUMN, pe, S_SIDE);
+      select(t, Lt);
     }
-    select(t, Lt);
     wait_pivot((int)(t & 1), t, host_wait);
     PivotResult r = piv_host_[t & 1];
     if (!r.found && opt_.pivot == PivotRule::Partial) {
@@ -664,31 +671,21 @@ bool Engine::factor_panel(int64_t v, bool wait_main, SolveStats& st, double& hos
     dev_.record(ev_pp_[par][j], S_SIDE);
     dbg_sync();
   }
-  chunk_pipeline(v, wait_main);
   return true;
 }
 
-// COMM stream: for every column chunk (in the order MAIN will consume them) and every step of
-// panel v, the owner of s_t forms R_t[chunk] = H_t (X[s_t, chunk] + Lrow_t R_prev[chunk]) outside
-// the panel's columns (those come from the panel piece, later panel blocks zeroed), and the row
-// segments are broadcast.  Consecutive segments with the same root go out as one RCCL group; a
-// segment whose owner needs earlier segments of other roots waits for their broadcast first.
-void Engine::chunk_pipeline(int64_t v, bool wait_main) {
+// Panel v's pivot rows over the next panel's block columns (LA_[par], step-major, ld wla), formed
+// by their owners and broadcast on their own: MAIN's look-ahead update of panel v+1 needs only
+// these, so the next pivot chain starts after a (q*m) x (qn*m) broadcast instead of after a whole
+// chunk's.  The chunk pass broadcasts these columns again with the rest of their chunk (MAIN's
+// chunk update skips them).
+void Engine::lookahead_rows(int64_t v, bool wait_main) {
   const int par = (int)(v & 1);
   const int64_t m = L_.m, npad = L_.npad;
-  const int64_t t0 = panel_t0(v), q = panel_q(v);
+  const int64_t q = panel_q(v);
   const size_t es = esz();
-  const int64_t C = (int64_t)cb0_.size();
-  const bool has_next = (v + 1 < npanels());
-  const int64_t start = has_next ? chunk_of_[panel_t0(v + 1)] : 0;
-  const int64_t pc0 = t0 * m, pc1 = (t0 + q) * m;  // panel columns
-  dev_.wait(S_COMM, ev_pp_[par][q - 1]);  // all panel pieces, multiplier rows and H_t (SIDE)
-  cur_phase_ = "pivot-row broadcast";
-  if (has_next) {
-    // The next panel's block columns first, on their own (LA_[par], step-major, ld wla): MAIN's
-    // look-ahead update of panel v+1 needs only these, so the next pivot chain starts after a
-    // (q*m) x (qn*m) broadcast instead of after a whole chunk's.  The chunk pass below broadcasts
-    // these columns again with the rest of their chunk (MAIN's chunk update skips them).
+  cur_phase_ = "look-ahead rows";
+  if (v + 1 < npanels()) {
     const int64_t xa = panel_t0(v + 1) * m, wla = panel_q(v + 1) * m;
     // at p > 1 on SIDE, right behind the panel pieces, with SIDE's communicator: emulated N = 16384
     // p = 4 at 50 GB/s per link 0.0588 -> 0.0564 s (80 % of the transfer hidden), p = 8 0.0430 ->
@@ -696,6 +693,7 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
     const bool la_side = L_.p > 1;
     const int ls = la_side ? S_SIDE : S_COMM;
     void* Tl = la_side ? T2_ : T_;
+    if (!la_side) dev_.wait(S_COMM, ev_pp_[par][q - 1]);  // panel pieces, Lrow, H_t (SIDE)
     if (wait_main) dev_.wait(ls, ev_c_[chunk_of_[panel_t0(v + 1)]]);
     std::vector<BcastOp> lops;
     auto lflush = [&]() {
@@ -735,6 +733,24 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
     lflush();
     dev_.record(ev_la_[par], ls);
   }
+}
+
+// COMM stream: for every column chunk (in the order MAIN will consume them) and every step of
+// panel v, the owner of s_t forms R_t[chunk] = H_t (X[s_t, chunk] + Lrow_t R_prev[chunk]) outside
+// the panel's columns (those come from the panel piece, later panel blocks zeroed), and the row
+// segments are broadcast.  Consecutive segments with the same root go out as one RCCL group; a
+// segment whose owner needs earlier segments of other roots waits for their broadcast first.
+void Engine::chunk_pipeline(int64_t v, bool wait_main) {
+  const int par = (int)(v & 1);
+  const int64_t m = L_.m, npad = L_.npad;
+  const int64_t t0 = panel_t0(v), q = panel_q(v);
+  const size_t es = esz();
+  const int64_t C = (int64_t)cb0_.size();
+  const bool has_next = (v + 1 < npanels());
+  const int64_t start = has_next ? chunk_of_[panel_t0(v + 1)] : 0;
+  const int64_t pc0 = t0 * m, pc1 = (t0 + q) * m;  // panel columns
+  dev_.wait(S_COMM, ev_pp_[par][q - 1]);  // all panel pieces, multiplier rows and H_t (SIDE)
+  cur_phase_ = "pivot-row broadcast";
   for (int64_t i = 0; i < C; ++i) {
     const int64_t c = (start + i) % C;
     const int64_t c0 = cb0_[c] * m, c1 = cb1_[c] * m, W = c1 - c0;
@@ -801,42 +817,47 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
   dbg_sync();
 }
 
-// MAIN stream: the depth-q trailing update of panel u.  The next panel's block columns are done
-// first (look-ahead) so its pivot search can start; then every other chunk, each behind the event
-// of its broadcast.  Hazards across streams: the multiplier panels are triple-buffered
-// (At_[u % 3]); Rb_[par] chunk c is rewritten by the COMM stream only after ev_c_[c] of the
-// following panel.
-void Engine::big_update(int64_t u) {
+// MAIN stream, first part of panel u's depth-q trailing update: the next panel's block columns
+// (look-ahead) so its pivot search can start; big_update() then does every other chunk.
+void Engine::lookahead_update(int64_t u) {
   const int par = (int)(u & 1);
-  void* At = At_[u % 3];
-  void* At_next = At_[(u + 1) % 3];
   const int64_t m = L_.m, rows = L_.rows, npad = L_.npad;
-  const int64_t t0 = panel_t0(u), q = panel_q(u), K = q * m;
-  const int64_t C = (int64_t)cb0_.size();
-  const bool has_next = (u + 1 < npanels());
-  const GemmExtra prows = pivot_rows_extra(par, q);
+  const int64_t q = panel_q(u), K = q * m;
   dev_.wait(S_MAIN, ev_edit_[par]);
-  int64_t x0 = -1, x1 = -1;  // look-ahead columns
-  if (has_next) {
-    const int64_t tn = panel_t0(u + 1), qn = panel_q(u + 1), cn = chunk_of_[tn];
+  if (u + 1 < npanels()) {
+    const int64_t tn = panel_t0(u + 1), qn = panel_q(u + 1);
     const int ms = S_MAIN;
-    x0 = tn * m;
-    x1 = (tn + qn) * m;
-    (void)cn;
-    // the look-ahead rows of panel u (chunk_pipeline): N = 16384 emulated p = 4 / 8 at 50 GB/s per
+    const int64_t x0 = tn * m, x1 = (tn + qn) * m;
+    const GemmExtra prows = pivot_rows_extra(par, q);
+    // the look-ahead rows of panel u (lookahead_rows): N = 16384 emulated p = 4 / 8 at 50 GB/s per
     // link 0.0669 -> 0.0595 s / 0.0485 -> 0.0431 s against waiting for the whole first chunk
     // (profiles/emu_direct_r3.md)
     dev_.wait(ms, ev_la_[par]);
     const int pe = prof_begin(ms);
     if (rows > 0) {
-      dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, x1 - x0, K, At, rows, LA_[par], x1 - x0,
-                elem(X_, x0), npad, ms, prows);
-      dev_.extract_neg_t(opt_.dtype, At_next, rows, X_, npad, rows, x0, m, ms);
+      dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, x1 - x0, K, At_[u % 3], rows, LA_[par],
+                x1 - x0, elem(X_, x0), npad, ms, prows);
+      dev_.extract_neg_t(opt_.dtype, At_[(u + 1) % 3], rows, X_, npad, rows, x0, m, ms);
     }
     prof_end(PH_UPDATE, pe, ms);
     dev_.record(ev_L_, ms);
     dbg_sync();
   }
+}
+
+// MAIN stream: the rest of panel u's trailing update, every chunk behind the event of its
+// broadcast.  Hazards across streams: the multiplier panels are triple-buffered (At_[u % 3]);
+// Rb_[par] chunk c is rewritten by the COMM stream only after ev_c_[c] of the following panel.
+void Engine::big_update(int64_t u) {
+  const int par = (int)(u & 1);
+  void* At = At_[u % 3];
+  const int64_t m = L_.m, rows = L_.rows, npad = L_.npad;
+  const int64_t t0 = panel_t0(u), q = panel_q(u), K = q * m;
+  const int64_t C = (int64_t)cb0_.size();
+  const bool has_next = (u + 1 < npanels());
+  const GemmExtra prows = pivot_rows_extra(par, q);
+  const int64_t x0 = has_next ? panel_t0(u + 1) * m : -1;  // look-ahead columns (done)
+  const int64_t x1 = has_next ? (panel_t0(u + 1) + panel_q(u + 1)) * m : -1;
   const int64_t start = has_next ? chunk_of_[panel_t0(u + 1)] : 0;
   const int64_t pc0 = t0 * m, pc1 = (t0 + q) * m;
   for (int64_t i = 0; i < C; ++i) {
@@ -921,11 +942,23 @@ SolveStats Engine::solve_steps() {
   // prologue: column 0, pivot searches of panel 0
   if (rows > 0) dev_.extract_neg_t(opt_.dtype, At_[0], rows, X_, npad, rows, 0, m, S_MAIN);
   dev_.record(ev_L_, S_MAIN);
-  ok = factor_panel(0, /*wait_main=*/false, st, host_wait);
+  begin_panel(0);
+  ok = factor_panel(0, st, host_wait);
 
+  // Per panel: the look-ahead rows and the chunk pass (SIDE / COMM), MAIN's look-ahead update and
+  // the rest of the trailing update, then the next panel's pivot chain.  (Enqueueing the next
+  // panel's first pivot search before the chunk pass was measured neutral: N = 8192 / 16384 /
+  // 32768 and emulated p = 4 / 8 at N = 16384 within 0.5 % -- profiles/side_chain_r3.md.)
   for (int64_t u = 0; ok && u < npanels(); ++u) {
+    const bool has_next = u + 1 < npanels();
+    lookahead_rows(u, /*wait_main=*/u > 0);
+    chunk_pipeline(u, /*wait_main=*/u > 0);
+    lookahead_update(u);
     big_update(u);
-    if (u + 1 < npanels()) ok = factor_panel(u + 1, /*wait_main=*/true, st, host_wait);
+    if (has_next) {
+      begin_panel(u + 1);
+      ok = factor_panel(u + 1, st, host_wait);
+    }
   }
   if (!ok) {
     comm_.drain_all(dev_);
