@@ -11,6 +11,9 @@ its corner, ``glob_time: %.2f`` (max over ranks), ``inverse matrix:`` + blank li
 corner, ``residual: %e`` (or ``p == 1!`` with ``--residual compat`` on one rank).  Exit codes:
 0 ok, 1 usage, 2 any failure (cannot open / cannot read / singular matrix / not enough memory).
 The in-process ``build/gj`` binary is the same contract with threads instead of processes.
+``--comm-timeout S``: a rank waiting longer than S seconds on a peer fails (every rank, naming the
+step, phase and collective).  ``--same-gpu``: rehearse the p-rank RCCL path with every rank on
+GPU 0 (each rank its own RCCL host over loopback sockets; functional check, not a timing).
 """
 from __future__ import annotations
 
@@ -62,6 +65,7 @@ def main(argv=None) -> int:
     ap.add_argument("--comm-timeout", type=float, default=600.0)
     ap.add_argument("--bcast", choices=["auto", "ring", "direct"], default=None)
     ap.add_argument("--json", action="store_true")
+    ap.add_argument("--same-gpu", action="store_true")
     try:
         args, unknown = ap.parse_known_args(argv)
     except SystemExit:
@@ -89,20 +93,31 @@ def main(argv=None) -> int:
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.same_gpu:
+        # rehearsal of the p-rank RCCL path on ONE GPU (as bench.py --same-gpu): every rank is its
+        # own RCCL "host", so RCCL accepts the shared device and connects the ranks by sockets
+        local = 0
+        os.environ["NCCL_HOSTID"] = f"gj-cli-rank{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29541")
+    from datetime import timedelta
+
+    pg_timeout = timedelta(seconds=max(60.0, args.comm_timeout))
     if gpu:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world,
+                                timeout=pg_timeout)
     else:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=pg_timeout)
     out = (lambda s: print(s, end="", flush=True)) if rank == 0 else (lambda s: None)
     nm = min(n, args.print_max)
     try:
         try:
             solver = DistributedGaussJordan(n, m, dtype=args.dtype, chunk_cols=args.chunk_cols, eps=args.eps,
                                             host_threads=args.host_threads, depth=args.depth, pivot=args.pivot,
-                                            local_rank=local if gpu else None)
+                                            local_rank=local if gpu else None, comm_timeout=args.comm_timeout)
         except C.GJError as e:  # agreed on every rank inside the constructor
             out("Not enough memory!\n" if e.status == 2 else f"error: {e}\n")
             return 2
@@ -118,7 +133,15 @@ def main(argv=None) -> int:
         else:
             solver.generate(args.gen, args.seed)
         out("A\n" + _corner(solver.corner(nm, "input")))
-        st = solver.solve()
+        try:
+            st = solver.solve()
+        except C.GJError as e:
+            if e.status != 6:  # not a communication failure
+                raise
+            # a peer died or hung: every rank names its step, phase and collective (Engine::solve)
+            # and leaves at once -- tearing the process group down could block on the dead peer
+            print(f"gj: rank {rank}: {e}", file=sys.stderr, flush=True)
+            os._exit(2)
         if st["status"] != 0:
             out("singular matrix\n" if st["status"] == 1 else
                 "not enough memory for block\n" if st["status"] == 7 else f"unknown error: {st['status']}\n")

@@ -106,7 +106,7 @@ class DistributedGaussJordan:
 
     def __init__(self, n: int, m: int, dtype: str = "fp64", chunk_cols: int = 0, eps: float = 1e-15,
                  sync_debug: bool = False, host_threads: int = 0, local_rank: Optional[int] = None,
-                 depth: int = 0, pivot: str = "block-min-inv-norm"):
+                 depth: int = 0, pivot: str = "block-min-inv-norm", comm_timeout: float = 600.0):
         C = load_native()
         if not dist.is_initialized():
             raise RuntimeError("torch.distributed is not initialised")
@@ -129,8 +129,10 @@ class DistributedGaussJordan:
             self.local_rank = None
             self.device = C.host_device(host_threads)
             self.comm = C.py_comm(TorchDistComm(), self.rank, self.world) if self.world > 1 else C.self_comm()
+        # comm_timeout: seconds any wait on a peer may take before every rank fails with the step,
+        # phase and collective it was in (Engine::solve), instead of hanging
         self.engine = C.Engine(self.device, self.comm, self.n, self.m, dtype, chunk_cols, eps, sync_debug, depth,
-                               pivot=pivot)
+                               comm_timeout_s=float(comm_timeout), pivot=pivot)
         self.layout = Layout(self.n, self.m, self.world, self.rank)
         self._rows = global_rows(self.n, self.m, self.world, self.rank)
 

@@ -115,3 +115,20 @@ def test_distributed_load_file_share_only(tmp_path):
         assert peak < 0.75 * full, (rank, peak / 2**20)
         print(f"rank {rank}: peak RSS growth while reading {peak / 2**20:.1f} MiB (share {len(rows) * n * 8 / 2**20:.1f} MiB)")
         assert status == 0 and res < 1e-7
+
+
+def test_torchrun_cli_hang_fails_fast():
+    """`--comm-timeout`: a rank that never joins the pivot exchange of step 3 (GJ_TEST_HANG) makes
+    the torchrun CLI job fail within the timeout, naming the step."""
+    import time
+    t0 = time.monotonic()
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1", GJ_TEST_HANG="1:3")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "-m", "mpi_jordan_crazy_acceleration_amd.cli", "--device", "cpu", "--comm-timeout", "5", "64", "8"]
+    r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    # the rank that waits in vain names the step; torchrun then stops the job (its peer may be
+    # terminated before it prints: torchrun ends the other workers when one fails)
+    assert "gj: rank 1: rank 1/2, step 3 of 8, phase pivot search: timed out after 5" in r.stderr, r.stderr[-3000:]
+    assert time.monotonic() - t0 < 90

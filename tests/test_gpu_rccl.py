@@ -62,3 +62,29 @@ def test_rccl_multi_rank_same_gpu(ranks, bcast):
     assert rep["residual_inf"] < 1e-6  # random 2048 x 2048: 2.7e-8
     assert abs(rep["residual_inf"] - one["residual_inf"]) <= 1e-3 * one["residual_inf"]
     assert len(rep["rank_solve_seconds_max"]) == ranks
+
+
+def _cli(nproc, *args, timeout=300):
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env["PYTHONPATH"] = ROOT
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "--local-ranks-filter", "0",
+           "-m", "mpi_jordan_crazy_acceleration_amd.cli", "--device", "gpu", "--comm-timeout", "60", *args]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert out.returncode == 0, out.stderr[-3000:]
+    return [l for l in out.stdout.splitlines() if not l.startswith("glob_time")]
+
+
+def test_torchrun_cli_two_ranks_same_gpu():
+    """The user-facing torchrun CLI at p = 2 (torch's RCCL process group + the engine's two RCCL
+    communicators, both ranks on GPU 0 as separate RCCL hosts): the reference's stdout contract
+    with the p = 1 corners and a small residual."""
+    one = _cli(1, "1024", "64")
+    two = _cli(2, "--same-gpu", "1024", "64")
+    assert two[:-1] == one[:-1]  # A and inverse corners (2 decimals), "inverse matrix:"
+    assert two[-1].startswith("residual: ") and float(two[-1].split()[1]) < 1e-8
