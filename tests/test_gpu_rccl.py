@@ -87,4 +87,5 @@ def test_torchrun_cli_two_ranks_same_gpu():
     one = _cli(1, "1024", "64")
     two = _cli(2, "--same-gpu", "1024", "64")
     assert two[:-1] == one[:-1]  # A and inverse corners (2 decimals), "inverse matrix:"
-    assert two[-1].startswith("residual: ") and float(two[-1].split()[1]) < 1e-8
+    r1, r2 = float(one[-1].split()[1]), float(two[-1].split()[1])
+    assert two[-1].startswith("residual: ") and r2 < 1e-6 and r2 <= 10 * r1 + 1e-12
