@@ -221,6 +221,7 @@ class Engine {
   int d_ = 1;
   std::string bcast_algo_ = "ring";
   bool comm_small_tiles_ = false;  // COMM chunk-normalisation GEMMs on the small latency tile
+  bool la_update_side_ = false;  // MAIN's look-ahead update of the next panel's columns on SIDE
   int bi_hint_ = -1;               // candidate-inverse kernel family (Device::set_block_inverse_hint)
   int reserved_cus_ = 0;
   double norm_a_ = -1;
@@ -277,6 +278,7 @@ class Engine {
   int ev_L_ = -1, ev_main_ = -1, ev_sel_[2] = {-1, -1}, ev_edit_[2] = {-1, -1};
   int ev_pp_[2][kMaxDepth] = {};
   int ev_la_[2] = {-1, -1};            // LA_[par] formed and broadcast (COMM)
+  int ev_cp_[2] = {-1, -1};            // chunk pass of a panel of that parity done (COMM)
   std::vector<int> ev_c_;        // per chunk: MAIN finished the panel update of that chunk
   std::vector<int> ev_b_[2];     // per chunk: all stacked rows of that chunk broadcast
   std::vector<int> pev_pool_;    // profiling events (timing enabled), reused across solves

@@ -177,6 +177,7 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // only where the pivot chain dominates (padded order <= 8192).  GJ_COMM_SMALL_TILES overrides.
   comm_small_tiles_ = L_.npad <= 8192;
   if (const char* e = std::getenv("GJ_COMM_SMALL_TILES")) comm_small_tiles_ = std::atoi(e) != 0;
+  if (const char* e = std::getenv("GJ_LA_UPDATE")) la_update_side_ = std::string(e) == "side";  // TEMP A/B
 
 }
 
@@ -298,6 +299,7 @@ void Engine::alloc_work(int64_t wmax) {
     ev_edit_[i] = dev_.create_event();
     for (int j = 0; j < kMaxDepth; ++j) ev_pp_[i][j] = dev_.create_event();
     ev_la_[i] = dev_.create_event();
+    ev_cp_[i] = dev_.create_event();
     for (size_t c = 0; c < cb0_.size(); ++c) ev_b_[i].push_back(dev_.create_event());
   }
   for (size_t c = 0; c < cb0_.size(); ++c) ev_c_.push_back(dev_.create_event());
@@ -563,6 +565,9 @@ void Engine::begin_panel(int64_t v) {
   cur_step_ = panel_t0(v);
   cur_phase_ = "pivot search";
   dev_.wait(S_SIDE, ev_L_);
+  // this panel's steps rewrite Lrow_ / Ht_ / PP_[v & 1], which the COMM chunk pass of panel v - 2
+  // reads (explicit: with the look-ahead update on SIDE nothing else orders the two)
+  if (v >= 2) dev_.wait(S_SIDE, ev_cp_[v & 1]);
   select(panel_t0(v), At_[v % 3]);
 }
 
@@ -814,6 +819,7 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
     flush();
     dev_.record(ev_b_[par][c], S_COMM);
   }
+  dev_.record(ev_cp_[par], S_COMM);
   dbg_sync();
 }
 
@@ -826,7 +832,7 @@ void Engine::lookahead_update(int64_t u) {
   dev_.wait(S_MAIN, ev_edit_[par]);
   if (u + 1 < npanels()) {
     const int64_t tn = panel_t0(u + 1), qn = panel_q(u + 1);
-    const int ms = S_MAIN;
+    const int ms = la_update_side_ ? S_SIDE : S_MAIN;
     const int64_t x0 = tn * m, x1 = (tn + qn) * m;
     const GemmExtra prows = pivot_rows_extra(par, q);
     // the look-ahead rows of panel u (lookahead_rows): N = 16384 emulated p = 4 / 8 at 50 GB/s per

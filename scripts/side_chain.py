@@ -6,7 +6,7 @@ each block-inverse dispatch and report, per kernel kind, the mean time per step 
 and the mean idle gap before it (waiting for the host's enqueue, for an event of another stream,
 or for free CUs).  The sum is the per-step chain length.
 
-    python scripts/side_chain.py gpurun_out/prof_x/run_results.db [steps]
+    python scripts/side_chain.py gpurun_out/prof_x/run_results.db [steps [depth]]
 """
 import collections
 import sqlite3
@@ -22,7 +22,7 @@ def short(name):
     return n[-40:]
 
 
-def main(db, nsteps=None):
+def main(db, nsteps=None, depth=0):
     con = sqlite3.connect(db)
     rows = con.execute("select name, start, end, stream_id, grid_x/workgroup_x from kernels order by start").fetchall()
     bi = [r for r in rows if "block_inverse" in r[0]]
@@ -58,6 +58,21 @@ def main(db, nsteps=None):
         tb += a[1]
         tg += a[2]
     print(f"| **total** | | **{tb / n:.1f}** | **{tg / n:.1f}** |")
+    if depth:
+        # wait before each step's block inverse, by the step's position in its panel (position 0
+        # waits for MAIN's look-ahead update, later ones only for this stream's own work)
+        pos = collections.defaultdict(list)
+        prev = None
+        for r in sel:
+            if "block_inverse" in r[0] and prev is not None:
+                i = starts.index(r[1]) if r[1] in starts else None
+                if i is not None:
+                    pos[i % depth].append((r[1] - prev) / 1e3)
+            prev = r[2]
+        print("\n| step in panel | idle before block_inverse, mean us |")
+        print("|---|---|")
+        for j in sorted(pos):
+            print(f"| {j} | {sum(pos[j]) / len(pos[j]):.1f} |")
     others = collections.defaultdict(float)
     for r in rows:
         if r[3] != side and t0 <= r[1] <= t1:
@@ -68,4 +83,4 @@ def main(db, nsteps=None):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else None)
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else None, int(sys.argv[3]) if len(sys.argv) > 3 else 0)
