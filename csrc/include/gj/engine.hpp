@@ -221,7 +221,6 @@ class Engine {
   int d_ = 1;
   std::string bcast_algo_ = "ring";
   bool comm_small_tiles_ = false;  // COMM chunk-normalisation GEMMs on the small latency tile
-  bool la_update_side_ = false;  // MAIN's look-ahead update of the next panel's columns on SIDE
   int bi_hint_ = -1;               // candidate-inverse kernel family (Device::set_block_inverse_hint)
   int reserved_cus_ = 0;
   double norm_a_ = -1;

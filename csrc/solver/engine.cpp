@@ -177,7 +177,6 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // only where the pivot chain dominates (padded order <= 8192).  GJ_COMM_SMALL_TILES overrides.
   comm_small_tiles_ = L_.npad <= 8192;
   if (const char* e = std::getenv("GJ_COMM_SMALL_TILES")) comm_small_tiles_ = std::atoi(e) != 0;
-  if (const char* e = std::getenv("GJ_LA_UPDATE")) la_update_side_ = std::string(e) == "side";  // TEMP A/B
 
 }
 
@@ -559,14 +558,15 @@ GemmExtra Engine::pivot_rows_extra(int par, int64_t nsteps) const {
   return ex;
 }
 
-// The pivot search of panel v's first step, enqueued on SIDE behind MAIN's look-ahead (event
-// ev_L_: column t0 extracted into At[v % 3] segment 0).
+// The pivot search of panel v's first step, enqueued on SIDE behind the look-ahead update (event
+// ev_L_: column t0 extracted into At[v % 3] segment 0; SIDE itself, or MAIN for panel 0).
 void Engine::begin_panel(int64_t v) {
   cur_step_ = panel_t0(v);
   cur_phase_ = "pivot search";
   dev_.wait(S_SIDE, ev_L_);
   // this panel's steps rewrite Lrow_ / Ht_ / PP_[v & 1], which the COMM chunk pass of panel v - 2
-  // reads (explicit: with the look-ahead update on SIDE nothing else orders the two)
+  // reads (with the look-ahead update on SIDE nothing else orders the two; the asynchronous
+  // virtual-rank test, tests/test_async_ranks.py, fails without this wait)
   if (v >= 2) dev_.wait(S_SIDE, ev_cp_[v & 1]);
   select(panel_t0(v), At_[v % 3]);
 }
@@ -680,7 +680,7 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
 }
 
 // Panel v's pivot rows over the next panel's block columns (LA_[par], step-major, ld wla), formed
-// by their owners and broadcast on their own: MAIN's look-ahead update of panel v+1 needs only
+// by their owners and broadcast on their own: the look-ahead update of panel v+1 needs only
 // these, so the next pivot chain starts after a (q*m) x (qn*m) broadcast instead of after a whole
 // chunk's.  The chunk pass broadcasts these columns again with the rest of their chunk (MAIN's
 // chunk update skips them).
@@ -823,16 +823,24 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
   dbg_sync();
 }
 
-// MAIN stream, first part of panel u's depth-q trailing update: the next panel's block columns
-// (look-ahead) so its pivot search can start; big_update() then does every other chunk.
+// First part of panel u's depth-q trailing update: the next panel's block columns (look-ahead), so
+// its pivot search can start; big_update() then does every other chunk on MAIN.  The look-ahead
+// runs on SIDE, right behind the look-ahead rows, not on MAIN: it needs only MAIN's chunk of
+// panel u-1 that holds these columns (the look-ahead rows already waited for it), not the rest
+// of MAIN's queue.  Measured against MAIN (scripts/ab.sh, two repetitions): N = 8192 28.6 / 29.0
+// -> 27.8 / 27.9 ms, 16384 166.2 -> 163.0 ms, 32768 1137.5 -> 1135.3 ms; emulated p = 4,
+// N = 16384, direct 50 GB/s 0.0551 / 0.0554 -> 0.0525 / 0.0529 s; p = 8, N = 32768 0.1670 ->
+// 0.1625 s (profiles/side_chain_r3.md).  Hazards: At_[(u + 1) % 3] was last read by MAIN's
+// update of panel u-2, finished before that chunk of u-1; MAIN's chunk pass of panel u skips
+// these columns; Lrow_ / Ht_ / PP_ reuse is ordered by ev_cp_ (begin_panel).
 void Engine::lookahead_update(int64_t u) {
   const int par = (int)(u & 1);
   const int64_t m = L_.m, rows = L_.rows, npad = L_.npad;
   const int64_t q = panel_q(u), K = q * m;
-  dev_.wait(S_MAIN, ev_edit_[par]);
+  dev_.wait(S_MAIN, ev_edit_[par]);  // MAIN's chunk pass reads the edited multipliers
   if (u + 1 < npanels()) {
     const int64_t tn = panel_t0(u + 1), qn = panel_q(u + 1);
-    const int ms = la_update_side_ ? S_SIDE : S_MAIN;
+    const int ms = S_SIDE;
     const int64_t x0 = tn * m, x1 = (tn + qn) * m;
     const GemmExtra prows = pivot_rows_extra(par, q);
     // the look-ahead rows of panel u (lookahead_rows): N = 16384 emulated p = 4 / 8 at 50 GB/s per
@@ -951,12 +959,20 @@ SolveStats Engine::solve_steps() {
   begin_panel(0);
   ok = factor_panel(0, st, host_wait);
 
-  // Per panel: the look-ahead rows and the chunk pass (SIDE / COMM), MAIN's look-ahead update and
-  // the rest of the trailing update, then the next panel's pivot chain.  (Enqueueing the next
-  // panel's first pivot search before the chunk pass was measured neutral: N = 8192 / 16384 /
-  // 32768 and emulated p = 4 / 8 at N = 16384 within 0.5 % -- profiles/side_chain_r3.md.)
+  // Per panel: the look-ahead rows and the chunk pass (SIDE / COMM), the look-ahead update (SIDE)
+  // and the rest of the trailing update (MAIN), then the next panel's pivot chain.
+  static const bool early = std::getenv("GJ_EARLY") != nullptr;  // TEMP A/B
   for (int64_t u = 0; ok && u < npanels(); ++u) {
     const bool has_next = u + 1 < npanels();
+    if (early) {
+      lookahead_rows(u, /*wait_main=*/u > 0);
+      lookahead_update(u);
+      if (has_next) begin_panel(u + 1);
+      chunk_pipeline(u, /*wait_main=*/u > 0);
+      big_update(u);
+      if (has_next) ok = factor_panel(u + 1, st, host_wait);
+      continue;
+    }
     lookahead_rows(u, /*wait_main=*/u > 0);
     chunk_pipeline(u, /*wait_main=*/u > 0);
     lookahead_update(u);
