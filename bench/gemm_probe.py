@@ -26,15 +26,18 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--check", action="store_true", help="compare one call against torch fp64")
     ap.add_argument("--op", default="acc", choices=["acc", "store"], help="C += A B or C = A B")
+    ap.add_argument("--lda", type=int, default=0, help="row stride of A^T (default M)")
+    ap.add_argument("--ldb", type=int, default=0, help="row stride of B (default N)")
+    ap.add_argument("--ldc", type=int, default=0, help="row stride of C (default N; the solver's is the padded order)")
     a = ap.parse_args()
     M, N, K = a.shape
     C_ = load_native()
     if a.variant:
         C_.set_gemm_variant(a.variant)
     dt = torch.float64 if a.dtype == "fp64" else torch.float32
-    At = torch.randn(K, M, dtype=dt, device="cuda")
-    B = torch.randn(K, N, dtype=dt, device="cuda")
-    C = torch.randn(M, N, dtype=dt, device="cuda")
+    At = torch.randn(K, max(a.lda, M), dtype=dt, device="cuda")[:, :M]
+    B = torch.randn(K, max(a.ldb, N), dtype=dt, device="cuda")[:, :N]
+    C = torch.randn(M, max(a.ldc, N), dtype=dt, device="cuda")[:, :N]
     err = None
     if a.check:
         C0 = C.clone()
@@ -50,6 +53,7 @@ def main():
     torch.cuda.synchronize()
     dt_s = (time.perf_counter() - t0) / a.reps
     print(json.dumps({"M": M, "N": N, "K": K, "dtype": a.dtype, "variant": a.variant or "default", "op": a.op,
+                      "lda": At.stride(0), "ldb": B.stride(0), "ldc": C.stride(0),
                       "ms": round(dt_s * 1e3, 4), "tflops": round(2.0 * M * N * K / dt_s / 1e12, 2), "rel_err": err}), flush=True)
 
 

@@ -961,18 +961,8 @@ SolveStats Engine::solve_steps() {
 
   // Per panel: the look-ahead rows and the chunk pass (SIDE / COMM), the look-ahead update (SIDE)
   // and the rest of the trailing update (MAIN), then the next panel's pivot chain.
-  static const bool early = std::getenv("GJ_EARLY") != nullptr;  // TEMP A/B
   for (int64_t u = 0; ok && u < npanels(); ++u) {
     const bool has_next = u + 1 < npanels();
-    if (early) {
-      lookahead_rows(u, /*wait_main=*/u > 0);
-      lookahead_update(u);
-      if (has_next) begin_panel(u + 1);
-      chunk_pipeline(u, /*wait_main=*/u > 0);
-      big_update(u);
-      if (has_next) ok = factor_panel(u + 1, st, host_wait);
-      continue;
-    }
     lookahead_rows(u, /*wait_main=*/u > 0);
     chunk_pipeline(u, /*wait_main=*/u > 0);
     lookahead_update(u);
