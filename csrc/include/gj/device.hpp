@@ -46,6 +46,11 @@ struct GemmExtra {
   // Few-tile GEMM on the panel-factorisation critical path: prefer small tiles (more workgroups,
   // shorter K loop per workgroup) over the throughput tiles of the trailing update.
   bool latency = false;
+  // Also write the result transposed and negated, tneg[c*ldtneg + r] = -C[r][c] for every output
+  // element (the K-major multiplier panel of the next pivot search, fused into the column update
+  // that produces it: one launch fewer on the pivot chain).  Register-staged tiles only.
+  void* tneg = nullptr;
+  int64_t ldtneg = 0;
 };
 
 // One product of a batched small-GEMM launch (Device::gemm_batch): C (+)= A B, A K-major.
@@ -134,6 +139,17 @@ class Device {
   virtual void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                              int32_t* valid, const int32_t* used, const Layout& L, double thresh,
                              int s) = 0;
+  // block_inverse with the pivot selection run by the launch's last workgroup (PivotSelectArgs:
+  // p > 1 the local argmin -> *sel.rec, like pivot_local; p == 1 the whole pivot_select_single).
+  // Returns false, having enqueued nothing, where the device or the kernel family it would use
+  // cannot fuse them; the caller then runs block_inverse and the selection as separate launches.
+  virtual bool block_inverse_select(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
+                                    int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                                    const PivotSelectArgs& sel, int s) {
+    (void)dt; (void)Lt; (void)ldl; (void)inv_t; (void)scores; (void)valid; (void)used; (void)L;
+    (void)thresh; (void)sel; (void)s;
+    return false;
+  }
   // Kernel family for the following block_inverse calls (-1 = the process default; 5 = the
   // co-resident form, which the engine picks where its pivot chain waits for whole CUs).  Devices
   // with a single implementation ignore it.

@@ -262,6 +262,7 @@ class Engine {
   int32_t* used_ = nullptr;
   int32_t* seq_ = nullptr;
   PivotRec* myrec_ = nullptr;
+  int32_t* sel_done_ = nullptr;  // workgroup counter of the fused candidate-inverse + selection launch
   PivotRec* recs_ = nullptr;
   PivotResult* piv_dev_ = nullptr;
   double* dscratch_ = nullptr;

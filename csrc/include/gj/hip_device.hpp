@@ -57,6 +57,9 @@ class HipDevice : public Device {
   void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                      int32_t* valid, const int32_t* used, const Layout& L, double thresh,
                      int s) override;
+  bool block_inverse_select(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
+                            int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                            const PivotSelectArgs& sel, int s) override;
   void set_block_inverse_hint(int variant) override { bi_hint_ = variant; }
   size_t block_inverse_scratch_bytes(DType dt, const Layout& L, int variant) const override;
   void prepare_block_inverse(DType dt, const Layout& L, int variant) override;

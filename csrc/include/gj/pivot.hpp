@@ -78,4 +78,22 @@ GJ_HD inline void pivot_commit(int32_t t, int32_t s, int32_t* pos, int32_t* phys
   seq[t] = s;
 }
 
+// Pivot selection fused into the candidate-inverse launch (Device::block_inverse_select): the
+// batch's last workgroup to finish (counted on *done, which it resets to 0) runs the local argmin
+// (p > 1: -> *rec, the record the all-gather sends) or, with one rank, the whole selection and
+// book-keeping (-> *rec, *out and the pinned host mirror), so the pivot chain loses a launch.
+struct PivotSelectArgs {
+  int32_t* done = nullptr;   // device counter, 0 between launches
+  int32_t t = 0;             // step
+  const int32_t* pos = nullptr;
+  int32_t* pos_w = nullptr;  // (p == 1: book-keeping arrays, written)
+  int32_t* phys_at = nullptr;
+  int32_t* used_w = nullptr;
+  int32_t* seq = nullptr;
+  PivotRec* rec = nullptr;
+  PivotResult* out = nullptr;       // p == 1 only
+  PivotResult* host_out = nullptr;  // p == 1 only
+  int32_t single = 0;               // 1: p == 1, the full selection
+};
+
 }  // namespace gj

@@ -805,6 +805,14 @@ size_t block_inverse_iscratch_bytes(const Layout& L) {
   return (size_t)L.nblk * 3 * L.m * sizeof(int);
 }
 
+bool block_inverse_select(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
+                          int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                          hipStream_t s, const PivotSelectArgs& sel, int variant) {
+  const int v = variant >= 0 ? variant : bi_variant();
+  if (v != 0 || L.nblk <= 0) return false;
+  return block_inverse_mfma(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, s, &sel);
+}
+
 void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                    int32_t* valid, const int32_t* used, const Layout& L, double thresh,
                    hipStream_t s, void* scratch, int* iscratch, int variant) {

@@ -35,6 +35,7 @@
 
 #include "kernels.hpp"
 #include "pivot_panel.hpp"
+#include "pivot_select.hpp"
 #include "wave_ops.hpp"
 
 namespace gj {
@@ -91,7 +92,7 @@ template <typename T, int MP, int LAY = 0>
 __global__ __launch_bounds__(64 * (MP / 16 + 1 + (LAY ? (MP / 16 - 1) / 3 : 0))) void block_inverse_mfma_kernel(
     const T* __restrict__ Lt, int64_t ldl, T* __restrict__ inv_t, double* __restrict__ scores,
     int32_t* __restrict__ valid, const int32_t* __restrict__ used, int m, int64_t p, int64_t k,
-    double thresh, int32_t* __restrict__ piv_out) {
+    double thresh, int32_t* __restrict__ piv_out, PivotSelectArgs sel) {
   using TL = BiTile<T>;
   using acc_t = typename TL::acc_t;
   constexpr int NW = MP / 16;     // block waves = row tiles = panels
@@ -107,9 +108,12 @@ __global__ __launch_bounds__(64 * (MP / 16 + 1 + (LAY ? (MP / 16 - 1) / 3 : 0)))
 
   const int b = blockIdx.x;
   if (used[(int64_t)b * p + k]) {
-    if (threadIdx.x == 0) {
-      valid[b] = 0;
-      scores[b] = 0.0;
+    if (threadIdx.x < 64) {
+      if (threadIdx.x == 0) {
+        valid[b] = 0;
+        scores[b] = 0.0;
+      }
+      select_tail(sel, scores, valid, used, gridDim.x, p, k);
     }
     return;
   }
@@ -377,6 +381,7 @@ __global__ __launch_bounds__(64 * (MP / 16 + 1 + (LAY ? (MP / 16 - 1) / 3 : 0)))
       }
       if (cc < m) redg[grp][cc] = csum;
       if (wave == 0) BIM_PROBE(1001);
+      __syncthreads();  // E3: the row sums are in LDS before the pivot wave reads them
     }
   }
   if (wave == NW) {
@@ -386,13 +391,17 @@ __global__ __launch_bounds__(64 * (MP / 16 + 1 + (LAY ? (MP / 16 - 1) / 3 : 0)))
         __syncthreads();  // E1(h)
         __syncthreads();  // E2(h)
       }
+      __syncthreads();  // E3
     }
   }
   (void)sing_exit;
   if (s_sing) {
-    if (tid == 0) {
-      valid[b] = 0;
-      scores[b] = 0.0;
+    if (wave == 0) {
+      if (lane == 0) {
+        valid[b] = 0;
+        scores[b] = 0.0;
+      }
+      select_tail(sel, scores, valid, used, gridDim.x, p, k);
     }
     return;
   }
@@ -409,6 +418,7 @@ __global__ __launch_bounds__(64 * (MP / 16 + 1 + (LAY ? (MP / 16 - 1) / 3 : 0)))
       scores[b] = mx;
       valid[b] = isfinite(mx) ? 1 : 0;
     }
+    select_tail(sel, scores, valid, used, gridDim.x, p, k);
   }
 }
 
@@ -418,18 +428,19 @@ int32_t* block_inverse_probe() { return g_piv_probe; }
 
 bool block_inverse_mfma(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                         int32_t* valid, const int32_t* used, const Layout& L, double thresh,
-                        hipStream_t s) {
+                        hipStream_t s, const PivotSelectArgs* sel) {
   const int m = (int)L.m;
   if (m <= 16 || m > 128) return false;
   const unsigned grid = (unsigned)L.nblk;
   if (grid == 0) return true;
   const int MP = m <= 32 ? 32 : m <= 64 ? 64 : 128;
+  const PivotSelectArgs tail = sel ? *sel : PivotSelectArgs{};
   // MP = 128: the pivot wave alone on its SIMD (LAY 1), where 8 block waves' MFMAs would share it:
   // 96.0 -> 86.4 us per batch of 64 fp64 128 x 128 candidates (MP = 64: no change, 9-wave layout)
 #define GJ_BI_LAUNCH(T, MPV, LAYV)                                                                       \
   hipLaunchKernelGGL((block_inverse_mfma_kernel<T, MPV, LAYV>), dim3(grid), dim3(64 * bim_hw_waves<MPV, LAYV>()), \
                      0, s, static_cast<const T*>(Lt), ldl, static_cast<T*>(inv_t), scores, valid, used, m, L.p,   \
-                     L.k, thresh, g_piv_probe)
+                     L.k, thresh, g_piv_probe, tail)
   if (dt == DType::F64) {
     if (MP == 32) GJ_BI_LAUNCH(double, 32, 0);
     else if (MP == 64) GJ_BI_LAUNCH(double, 64, 0);

@@ -140,6 +140,8 @@ struct GemmArgs {
   int nparts;
   bool latency;     // GemmExtra::latency -> CfgSmall for few-tile launches
   int group;        // LDS-DMA kernel: tile rows per column-walk group (1 = row-major tile order)
+  void* tneg;       // GemmExtra::tneg: -C^T also written here (register-staged tiles)
+  int64_t ldt;
 };
 
 // XCD-aware bijective remap: blocks b and b+8 share an XCD (MI355X_MICROARCH.md §Workgroup
@@ -334,6 +336,21 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, const int tile) {
           bstore(acc[i][j][q], rc, (r < Mt && c < Nt) ? cvoff + j * 16 * ES : kOOB, soff);
         }
       }
+    if (g.tneg) {  // -C^T: lanes 0-15 of a row group write 16 rows of the transpose, 4 consecutive
+      __amdgpu_buffer_rsrc_t rt = rsrc(static_cast<T*>(g.tneg) + n0 * g.ldt + m0);
+      const int ldt = (int)g.ldt;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = rlane + i * 16 + MF::rq(q);
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const int c = clane + j * 16;
+            bstore(-acc[i][j][q], rt, (r < Mt && c < Nt) ? (c * ldt + r) * ES : kOOB, 0);
+          }
+        }
+    }
   } else {  // MODE_RESID: per-row partial sum of |acc - I| over this wave's TN real columns
 #pragma unroll
     for (int i = 0; i < MI; ++i)
@@ -858,6 +875,7 @@ static void launch(const GemmArgs& a, hipStream_t s) {
     const bool deep = a.K >= 384 && big_tiles >= 512;
     v = deep ? 11 : 1;
   }
+  if (v == 11 && a.tneg) v = sizeof(T) == 8 ? 9 : 6;  // the LDS-DMA kernels have no -C^T epilogue
   if (v == 11) {  // LDS-DMA fp64 kernel; other dtypes / layouts / alignments take the next best tile
     if constexpr (sizeof(T) == 8 && AL == 1 && MODE != MODE_RESID) {
       if (glds_ok(a)) return launch_glds<MODE>(a, s);
@@ -882,6 +900,8 @@ static void fill_extra(GemmArgs& a, const GemmExtra* ex) {
   a.zh = ex ? ex->zh : 0;
   for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) a.zr[z] = (ex && z < ex->nzr) ? ex->zr[z] : kNone;
   a.latency = ex ? ex->latency : false;
+  a.tneg = ex ? ex->tneg : nullptr;
+  a.ldt = ex ? ex->ldtneg : 0;
 }
 
 void gemm(DType dt, int op, int a_kmajor, int64_t M, int64_t N, int64_t K, const void* A,
@@ -891,6 +911,8 @@ void gemm(DType dt, int op, int a_kmajor, int64_t M, int64_t N, int64_t K, const
   GemmArgs a{};
   a.M = M; a.N = N; a.K = K; a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.C = C; a.ldc = ldc;
   fill_extra(a, ex);
+  if (a.tneg && a.ldt * 128 * (dt == DType::F64 ? 8 : 4) >= kRecords)
+    throw Error(Status::BadArgs, "gemm: -C^T leading dimension too large for 32-bit buffer offsets");
   const int mode = op == 0 ? MODE_ACC : MODE_STORE;
 #define GJ_DISPATCH(T)                                                        \
   if (a_kmajor) {                                                             \

@@ -42,7 +42,13 @@ void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* s
 // blockinv_mfma.hip: 16 < m <= 128 (false = not handled)
 bool block_inverse_mfma(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                         int32_t* valid, const int32_t* used, const Layout& L, double thresh,
-                        hipStream_t s);
+                        hipStream_t s, const PivotSelectArgs* sel = nullptr);
+// block_inverse with the pivot selection fused into the launch (PivotSelectArgs) where the kernel
+// family the call resolves to supports it (the matrix-core register kernel); false = nothing was
+// launched, the caller runs block_inverse and the selection separately
+bool block_inverse_select(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
+                          int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                          hipStream_t s, const PivotSelectArgs& sel, int variant = -1);
 // test probe: when set, the matrix-core block inverses write the pivot row of every column of
 // every candidate to piv_out[b * m + c] (device memory; nullptr = off)
 void set_block_inverse_probe(int32_t* piv_out);

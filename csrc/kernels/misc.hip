@@ -14,6 +14,7 @@
 
 #include "gj/gen.hpp"
 #include "kernels.hpp"
+#include "pivot_select.hpp"
 #include "wave_ops.hpp"
 
 namespace gj {
@@ -194,36 +195,6 @@ void h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, hipStrea
 }
 
 // ---------------------------------------------------------------- pivot selection
-// One wave: each lane scans every 64th candidate, then a 6-step shuffle tree (no LDS, no
-// workgroup barrier: this launch sits on the pivot chain once per step).  pivot_better is a strict
-// total order on valid records (distinct logical rows), so the tree shape cannot change the winner.
-__device__ PivotRec pivot_local_wave(const double* scores, const int32_t* valid, const int32_t* used,
-                                     const int32_t* pos, int64_t nblk, int64_t p, int64_t k) {
-  PivotRec best = pivot_invalid();
-  for (int64_t b = threadIdx.x; b < nblk; b += 64) {
-    const int64_t g = b * p + k;
-    if (used[g] || !valid[b]) continue;
-    PivotRec c;
-    c.score = scores[b];
-    c.logical = pos[g];
-    c.phys = (int32_t)g;
-    c.valid = 1;
-    c.pad_ = 0;
-    if (pivot_better(c, best, (int32_t)p)) best = c;
-  }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    PivotRec o;
-    o.score = __shfl_xor(best.score, off, 64);
-    o.logical = __shfl_xor(best.logical, off, 64);
-    o.phys = __shfl_xor(best.phys, off, 64);
-    o.valid = __shfl_xor(best.valid, off, 64);
-    o.pad_ = 0;
-    if (pivot_better(o, best, (int32_t)p)) best = o;
-  }
-  return best;
-}
-
 __global__ __launch_bounds__(64) void pivot_local_kernel(const double* scores, const int32_t* valid,
                                                          const int32_t* used, const int32_t* pos,
                                                          int64_t nblk, int64_t p, int64_t k,
@@ -236,40 +207,6 @@ void pivot_local(const double* scores, const int32_t* valid, const int32_t* used
                  const Layout& L, PivotRec* out, hipStream_t s) {
   hipLaunchKernelGGL(pivot_local_kernel, dim3(1), dim3(64), 0, s, scores, valid, used, pos, L.nblk,
                      L.p, L.k, out);
-}
-
-// Winner of the gathered records -> book-keeping, *out, and the host mirror (one thread).
-__device__ void pivot_finish(PivotRec best, int32_t p, int32_t t, int32_t* pos, int32_t* phys_at,
-                             int32_t* used, int32_t* seq, PivotResult* out, PivotResult* host_out) {
-  PivotResult r;
-  r.step = t;
-  r.pad_ = 0;
-  if (best.valid) {
-    r.found = 1;
-    r.phys = best.phys;
-    r.owner = best.phys % p;
-    r.logical = best.logical;
-    r.score = best.score;
-    pivot_commit(t, best.phys, pos, phys_at, used, seq);
-  } else {
-    r.found = 0;
-    r.phys = -1;
-    r.owner = -1;
-    r.logical = -1;
-    r.score = 0.0;
-  }
-  *out = r;
-  if (host_out) {  // the host polls `step`: every other field first, then a system-scope fence
-    volatile PivotResult* h = host_out;
-    h->found = r.found;
-    h->phys = r.phys;
-    h->owner = r.owner;
-    h->logical = r.logical;
-    h->score = r.score;
-    __threadfence_system();
-    h->step = r.step;
-    __threadfence_system();
-  }
 }
 
 __global__ void pivot_global_kernel(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos,

@@ -249,6 +249,15 @@ void HipDevice::block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t
   kern::block_inverse(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, hs(streams_[s]), sc, isc, variant);
   check_launch();
 }
+bool HipDevice::block_inverse_select(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
+                                     int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                                     const PivotSelectArgs& sel, int s) {
+  if (!kern::block_inverse_select(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, hs(streams_[s]), sel,
+                                  bi_hint_))
+    return false;
+  check_launch();
+  return true;
+}
 void HipDevice::candidate_maxabs(DType dt, const void* Lt, int64_t ldl, double* scores, int32_t* valid,
                                  const int32_t* used, const Layout& L, double thresh, int s) {
   kern::candidate_maxabs(dt, Lt, ldl, scores, valid, used, L, thresh, hs(streams_[s]));

@@ -281,6 +281,9 @@ void Engine::alloc_work(int64_t wmax) {
   used_ = static_cast<int32_t*>(dev_.alloc(sizeof(int32_t) * L_.Nr));
   seq_ = static_cast<int32_t*>(dev_.alloc(sizeof(int32_t) * L_.Nr));
   myrec_ = static_cast<PivotRec*>(dev_.alloc(sizeof(PivotRec)));
+  sel_done_ = static_cast<int32_t*>(dev_.alloc(sizeof(int32_t)));
+  dev_.memset0(sel_done_, sizeof(int32_t), S_SIDE);
+  dev_.sync_stream(S_SIDE);
   recs_ = static_cast<PivotRec*>(dev_.alloc(sizeof(PivotRec) * L_.p));
   piv_dev_ = static_cast<PivotResult*>(dev_.alloc(sizeof(PivotResult)));
   dscratch_ = static_cast<double*>(dev_.alloc(sizeof(double) * 64));
@@ -311,6 +314,7 @@ void Engine::free_work() {
                                reinterpret_cast<void**>(&valid_), reinterpret_cast<void**>(&pos_),
                                reinterpret_cast<void**>(&phys_at_), reinterpret_cast<void**>(&used_),
                                reinterpret_cast<void**>(&seq_), reinterpret_cast<void**>(&myrec_),
+                               reinterpret_cast<void**>(&sel_done_),
                                reinterpret_cast<void**>(&recs_), reinterpret_cast<void**>(&piv_dev_),
                                reinterpret_cast<void**>(&dscratch_), reinterpret_cast<void**>(&iscratch_)};
   for (int i = 0; i < 3; ++i) dptrs.push_back(&At_[i]);
@@ -517,23 +521,43 @@ void Engine::select(int64_t t, const void* Lt, bool full) {
     dev_.commit_candidate(opt_.dtype, inv_, inv1_, valid1_, myrec_, L_, S_SIDE);
     prof_end(PH_PIVOT, pe, S_SIDE);
   } else {
+    // The selection runs in the candidate-inverse launch's last workgroup where the kernel family
+    // supports it (one launch fewer on the pivot chain per step); otherwise as its own launch.
+    // One rank: the local record is the gathered set -> local argmin + book-keeping in one go; the
+    // result goes straight to pinned host memory (no copy kernel), the host polls its step field.
+    if (L_.p == 1) piv_host_[par].step = -1;
+    bool fused = false;
     if (L_.nblk > 0) {
       dev_.set_block_inverse_hint(bi_hint_);  // per call: a device may be shared with other users
-      dev_.block_inverse(opt_.dtype, Lt, L_.rows, inv_, scores_, valid_, used_, L_, thresh, S_SIDE);
+      PivotSelectArgs sa;
+      sa.done = sel_done_;
+      sa.t = (int32_t)t;
+      sa.pos = pos_;
+      sa.rec = myrec_;
+      if (L_.p == 1) {
+        sa.single = 1;
+        sa.pos_w = pos_;
+        sa.phys_at = phys_at_;
+        sa.used_w = used_;
+        sa.seq = seq_;
+        sa.out = piv_dev_;
+        sa.host_out = &piv_host_[par];
+      }
+      fused = dev_.block_inverse_select(opt_.dtype, Lt, L_.rows, inv_, scores_, valid_, used_, L_, thresh, sa,
+                                        S_SIDE);
+      if (!fused) dev_.block_inverse(opt_.dtype, Lt, L_.rows, inv_, scores_, valid_, used_, L_, thresh, S_SIDE);
       dev_.set_block_inverse_hint(-1);
     }
     if (L_.p == 1) {
-      // one rank: the local record is the gathered set -> local argmin + book-keeping in one launch;
-      // the result goes straight to pinned host memory (no copy kernel), the host polls its step field
-      piv_host_[par].step = -1;
-      dev_.pivot_select_single(scores_, valid_, L_, (int32_t)t, pos_, phys_at_, used_, seq_, myrec_,
-                               piv_dev_, &piv_host_[par], S_SIDE);
+      if (!fused)
+        dev_.pivot_select_single(scores_, valid_, L_, (int32_t)t, pos_, phys_at_, used_, seq_, myrec_,
+                                 piv_dev_, &piv_host_[par], S_SIDE);
       prof_end(PH_PIVOT, pe, S_SIDE);
       dev_.record(ev_sel_[par], S_SIDE);
       dbg_sync();
       return;
     }
-    dev_.pivot_local(scores_, valid_, used_, pos_, L_, myrec_, S_SIDE);
+    if (!fused) dev_.pivot_local(scores_, valid_, used_, pos_, L_, myrec_, S_SIDE);
     prof_end(PH_PIVOT, pe, S_SIDE);
   }
   if (hang_step_ == t) {  // GJ_TEST_HANG: this rank never joins the exchange of step t
@@ -590,11 +614,15 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
       dev_.wait(S_SIDE, ev_pp_[par][j - 1]);
       const int pe = prof_begin(S_SIDE);
       if (rows > 0) {
+        // the update writes the new multipliers -X[:, t]^T (segment j of At) as it stores X[:, t]:
+        // one launch fewer per step (emulated p = 4, N = 16384, direct 50 GB/s: 0.0533 / 0.0538 ->
+        // 0.0518 / 0.0518 s; neutral elsewhere, profiles/side_chain_r3.md)
         GemmExtra ex = pivot_rows_extra(par, j);
         ex.latency = true;
+        ex.tneg = Lt;
+        ex.ldtneg = rows;
         dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, m, j * m, At_[v % 3], rows,
                   elem(PP_[par], j * m), dm, elem(X_, t * m), npad, S_SIDE, ex);
-        dev_.extract_neg_t(opt_.dtype, Lt, rows, X_, npad, rows, t * m, m, S_SIDE);
       }
       prof_end(PH_COLUMN, pe, S_SIDE);
       select(t, Lt);

@@ -53,6 +53,31 @@ def test_generate_matches_numpy():
     assert np.array_equal(Xc[n:, n:], np.eye(Nr * m - n))
 
 
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("M,K,latency,variant", [(300, 256, True, "auto"), (4096, 384, True, "auto"),
+                                                 (1000, 512, False, "auto"), (777, 128, False, "glds"),
+                                                 (2048, 256, False, "big"), (513, 128, True, "narrow")])
+def test_gemm_tneg_epilogue(native, dtype, M, K, latency, variant):
+    """Column update with the fused multiplier write: C += A B and tneg = -C^T (bit-identical)."""
+    native.set_gemm_variant(variant)
+    try:
+        N = 128
+        At = _rand((K, M), dtype, 21).cuda()
+        B = _rand((K, N), dtype, 22).cuda()
+        C = _rand((M, N), dtype, 23)
+        ref = C.double() + At.cpu().double().t() @ B.cpu().double()
+        Cd = C.cuda()
+        T = torch.full((N, M + 8), 7.0, dtype=dtype, device="cuda")
+        ops.gemm(At, B, Cd, op="acc", a_kmajor=True, tneg=T[:, :M],
+                 latency=latency)
+        tol = (1e-12 if dtype == torch.float64 else 2e-5) * K
+        assert (Cd.cpu().double() - ref).abs().max().item() < tol
+        assert torch.equal(T[:, :M].cpu(), -Cd.cpu().t())
+        assert torch.equal(T[:, M:].cpu(), torch.full((N, 8), 7.0, dtype=dtype))
+    finally:
+        native.set_gemm_variant("auto")
+
+
 def test_extract_neg_t():
     X = _rand((300, 512), torch.float64, 5).cuda()
     Lt = ops.extract_neg_t(X, 128, 96)

@@ -154,6 +154,22 @@ def test_host_gemm_extras_match_torch():
     assert (C - ref).abs().max().item() < 1e-12
 
 
+def test_host_gemm_tneg_epilogue():
+    """Host executor: the column update's fused multiplier write, tneg = -C^T after C += A B."""
+    import torch
+    from mpi_jordan_crazy_acceleration_amd import ops
+    g = torch.Generator().manual_seed(4)
+    A = torch.rand(90, 20, generator=g, dtype=torch.float64)
+    B = torch.rand(20, 70, generator=g, dtype=torch.float64)
+    C = torch.rand(90, 70, generator=g, dtype=torch.float64)
+    ref = C + A @ B
+    T = torch.full((70, 96), 3.0, dtype=torch.float64)
+    ops.gemm(A.t().contiguous(), B, C, op="acc", a_kmajor=True, tneg=T[:, :90])
+    assert (C - ref).abs().max().item() < 1e-12
+    assert torch.equal(T[:, :90], -C.t())
+    assert torch.equal(T[:, 90:], torch.full((70, 6), 3.0, dtype=torch.float64))
+
+
 def test_python_solve_vector_native_path(native):
     import mpi_jordan_crazy_acceleration_amd as gj
     rng = np.random.default_rng(11)
