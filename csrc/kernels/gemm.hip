@@ -14,7 +14,7 @@
 // for fp64; v_mfma_f32_16x16x4_f32, row = 4*(lane>>4) + reg, or v_mfma_f32_32x32x2_f32 for fp32;
 // the accumulator is loaded straight from C in the C/D layout, so the read-modify-write needs no
 // separate epilogue pass):
-//   * gemm_glds_f64 — the fp64 trailing update (K = depth*m >= 384, enough tiles to fill the chip):
+//   * gemm_glds_f64 — the fp64 trailing update (K = depth*m >= 256, enough tiles to fill the chip):
 //     128 x 64 tile per 256-thread workgroup, 2 x 2 waves of 64 x 32, operands staged global -> LDS
 //     by LDS-DMA (buffer_load_dwordx4 ... lds) into a 2-stage ring, counted vmcnt + raw s_barrier,
 //     4 workgroups per CU (82 % MFMA busy at 2.3 GHz: profiles/gemm_variants_k512.md).
@@ -67,7 +67,7 @@ struct Cfg {
 // The tiles the solver selects (profiles/gemm_variants_k512.md; the round-1 tuning candidates
 // tall / narrowpf / square / wide / big8 / valu were measured slower everywhere and removed):
 using CfgBig = Cfg<128, 128, 16, 2, 4, 2>;   // 512 threads, 2 WG/CU: the residual GEMM
-using CfgNarrow = Cfg<128, 64, 8, 2, 2, 4>;  // 256 threads, 4 WG/CU: K < 384 trailing updates
+using CfgNarrow = Cfg<128, 64, 8, 2, 2, 4>;  // 256 threads, 4 WG/CU: shallow / narrow updates
 using CfgSmall = Cfg<64, 32, 16, 2, 1, 8>;   // 128 threads: latency-bound panel GEMMs (few tiles)
 using CfgSquarePf = Cfg<128, 128, 8, 2, 2, 2, 2>;  // fp32 deep trailing updates (110.5 TF/s)
 using CfgBigPf = Cfg<128, 128, 16, 2, 4, 2, 2>;    // fp64 deep updates the LDS-DMA kernel cannot take
@@ -868,11 +868,13 @@ static void launch(const GemmArgs& a, hipStream_t s) {
     return launch_cfg<T, AL, MODE, CfgSmall>(a, s);
   int v = gemm_variant();
   if (v == kAutoVariant) {
-    // Deep trailing updates (K >= 384) with enough 128x128 tiles to fill the chip: fp64 the LDS-DMA
-    // kernel (61 TF/s vs 57.6 register-staged at 32768x4096x512), fp32 the 64x64-per-wave square
-    // tile (110.5 TF/s).  Everything else keeps the register-staged narrow tile.
+    // Trailing updates (K >= 256) with enough 128x128 tiles to fill the chip: fp64 the LDS-DMA
+    // kernel (61 TF/s vs 57.6 register-staged at 32768x4096x512; at the depth-2 K = 256 of
+    // N = 8192 45.6 vs 43.1 TF/s at 8192x4096x256 and 26.9 vs 27.9 ms per inversion, round 3),
+    // fp32 (K >= 384, as measured) the LDS-DMA 32x32x2 kernel.  Everything else keeps the
+    // register-staged narrow tile.
     const int64_t big_tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
-    const bool deep = a.K >= 384 && big_tiles >= 512;
+    const bool deep = a.K >= (sizeof(T) == 8 ? 256 : 384) && big_tiles >= 512;
     v = deep ? 11 : 1;
   }
   if (v == 11 && a.tneg) v = sizeof(T) == 8 ? 9 : 6;  // the LDS-DMA kernels have no -C^T epilogue
