@@ -49,10 +49,9 @@ struct SolveOptions {
   DType dtype = DType::F64;
   int64_t chunk_cols = 0;   // pipelining granularity of the pivot-row broadcast (0 = auto)
   int depth = 0;            // elimination steps fused per trailing update (K = depth*m), 1..8;
-                            // 0 = auto: 2 up to N = 8192 and on p > 1 ranks of <= 2048 rows
-                            // (pivot-chain-bound); 8 on ranks of <= 4096 rows of a p > 1 job
-                            // with N > 16384 (p = 8 at N = 32768); else 4
-                            // (profiles/small_n_sweep.md, profiles/depth_pgt1.md)
+                            // 0 = auto: 2 up to N = 8192 (pivot-chain-bound); 8 on ranks of
+                            // <= 4096 rows of a p > 1 job with N > 16384 (p = 8 at N = 32768);
+                            // else 4 (profiles/small_n_sweep.md, profiles/depth_pgt1.md)
   double eps = kDefaultEps;
   PivotRule pivot = PivotRule::MinInvNorm;
   bool sync_debug = false;  // synchronise every stream after every phase (race screening)

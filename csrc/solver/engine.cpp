@@ -89,13 +89,8 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // boundaries the pivot chain must hide behind a short trailing update; emulated under the
   // communication-cost model 0.167 vs 0.177 s, while depth 6 / 8 lose at p = 1 / 2 / 4 and at
   // N = 16384: profiles/depth_pgt1.md)
-  // and 2 on ranks of <= 2048 rows (p = 8 at N = 16384: the rank's trailing update per step is
-  // shorter than its pivot chain; emulated under the direct 50 GB/s model depth 2 / 3 / 4 / 6
-  // 0.0382 / 0.0390 / 0.0408 / 0.0432 s, profiles/depth_pgt1.md)
   const bool small_rank = L_.p > 1 && L_.max_nblk * L_.m <= 4096;
-  const bool tiny_rank = L_.p > 1 && L_.max_nblk * L_.m <= 2048;
-  const int want = opt_.depth > 0 ? opt_.depth
-                                  : ((L_.npad <= 8192 || tiny_rank) ? 2 : (small_rank && L_.npad > 16384) ? 8 : 4);
+  const int want = opt_.depth > 0 ? opt_.depth : (L_.npad <= 8192 ? 2 : (small_rank && L_.npad > 16384) ? 8 : 4);
   d_ = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)want, (int64_t)kMaxDepth, L_.Nr}));
 
   // Column chunk plan: fixed partition of the Nr block columns into runs of a multiple of d blocks.
