@@ -46,11 +46,12 @@ struct GemmExtra {
   // Few-tile GEMM on the panel-factorisation critical path: prefer small tiles (more workgroups,
   // shorter K loop per workgroup) over the throughput tiles of the trailing update.
   bool latency = false;
-  // Also write the result transposed and negated, tneg[c*ldtneg + r] = -C[r][c] for every output
-  // element (the K-major multiplier panel of the next pivot search, fused into the column update
-  // that produces it: one launch fewer on the pivot chain).  Register-staged tiles only.
+  // Also write the result transposed and negated, tneg[c*ldtneg + r] = -C[r][c], for the output
+  // columns c < tneg_cols (0 = all): the K-major multiplier panel of the next pivot search, fused
+  // into the column update that produces it (one launch fewer on the pivot chain).
   void* tneg = nullptr;
   int64_t ldtneg = 0;
+  int64_t tneg_cols = 0;
 };
 
 // One product of a batched small-GEMM launch (Device::gemm_batch): C (+)= A B, A K-major.

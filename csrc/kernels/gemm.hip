@@ -140,8 +140,8 @@ struct GemmArgs {
   int nparts;
   bool latency;     // GemmExtra::latency -> CfgSmall for few-tile launches
   int group;        // LDS-DMA kernel: tile rows per column-walk group (1 = row-major tile order)
-  void* tneg;       // GemmExtra::tneg: -C^T also written here (register-staged tiles)
-  int64_t ldt;
+  void* tneg;       // GemmExtra::tneg: -C^T of the columns < tncols also written here
+  int64_t ldt, tncols;
 };
 
 // XCD-aware bijective remap: blocks b and b+8 share an XCD (MI355X_MICROARCH.md §Workgroup
@@ -336,9 +336,10 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, const int tile) {
           bstore(acc[i][j][q], rc, (r < Mt && c < Nt) ? cvoff + j * 16 * ES : kOOB, soff);
         }
       }
-    if (g.tneg) {  // -C^T: lanes 0-15 of a row group write 16 rows of the transpose, 4 consecutive
+    if (g.tneg && n0 < g.tncols) {  // -C^T: lanes 0-15 of a row group write 16 rows of the transpose
       __amdgpu_buffer_rsrc_t rt = rsrc(static_cast<T*>(g.tneg) + n0 * g.ldt + m0);
       const int ldt = (int)g.ldt;
+      const int Ntn = (int)((g.tncols - n0) < Nt ? (g.tncols - n0) : Nt);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -347,7 +348,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, const int tile) {
 #pragma unroll
           for (int j = 0; j < NJ; ++j) {
             const int c = clane + j * 16;
-            bstore(-acc[i][j][q], rt, (r < Mt && c < Nt) ? (c * ldt + r) * ES : kOOB, 0);
+            bstore(-acc[i][j][q], rt, (r < Mt && c < Ntn) ? (c * ldt + r) * ES : kOOB, 0);
           }
         }
     }
@@ -599,6 +600,22 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
         bstore(acc[i][j][q], rc, (r < Mt && c < Nt) ? cvoff + j * 16 * ES : kOOB, soff);
       }
     }
+  if (g.tneg && n0 < g.tncols) {  // -C^T of the columns < tncols (GemmExtra::tneg)
+    __amdgpu_buffer_rsrc_t rt = rsrc(static_cast<double*>(g.tneg) + n0 * g.ldt + m0);
+    const int ldt = (int)g.ldt;
+    const int Ntn = (int)((g.tncols - n0) < Nt ? (g.tncols - n0) : Nt);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = rlane + i * 16 + MF::rq(q);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int c = clane + j * 16;
+          bstore(-acc[i][j][q], rt, (r < Mt && c < Ntn) ? (c * ldt + r) * ES : kOOB, 0);
+        }
+      }
+  }
 }
 
 template <int MODE>
@@ -877,7 +894,7 @@ static void launch(const GemmArgs& a, hipStream_t s) {
     const bool deep = a.K >= (sizeof(T) == 8 ? 256 : 384) && big_tiles >= 512;
     v = deep ? 11 : 1;
   }
-  if (v == 11 && a.tneg) v = sizeof(T) == 8 ? 9 : 6;  // the LDS-DMA kernels have no -C^T epilogue
+  if (v == 11 && a.tneg && sizeof(T) == 4) v = 6;  // the fp32 LDS-DMA kernel has no -C^T epilogue
   if (v == 11) {  // LDS-DMA fp64 kernel; other dtypes / layouts / alignments take the next best tile
     if constexpr (sizeof(T) == 8 && AL == 1 && MODE != MODE_RESID) {
       if (glds_ok(a)) return launch_glds<MODE>(a, s);
@@ -904,6 +921,7 @@ static void fill_extra(GemmArgs& a, const GemmExtra* ex) {
   a.latency = ex ? ex->latency : false;
   a.tneg = ex ? ex->tneg : nullptr;
   a.ldt = ex ? ex->ldtneg : 0;
+  a.tncols = (ex && ex->tneg_cols > 0) ? ex->tneg_cols : (int64_t(1) << 62);
 }
 
 void gemm(DType dt, int op, int a_kmajor, int64_t M, int64_t N, int64_t K, const void* A,

@@ -65,8 +65,10 @@ void gemm_t(GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const T* A, 
         c[j] = (T)((zrow || (j >= ex.zc0 && j < ex.zc1) ? 0.0 : (double)c[j]) + acc[j]);
     else
       for (int64_t j = 0; j < N; ++j) c[j] = (T)acc[j];
-    if (ex.tneg)
-      for (int64_t j = 0; j < N; ++j) static_cast<T*>(ex.tneg)[j * ex.ldtneg + i] = -c[j];
+    if (ex.tneg) {
+      const int64_t nt = ex.tneg_cols > 0 ? std::min(ex.tneg_cols, N) : N;
+      for (int64_t j = 0; j < nt; ++j) static_cast<T*>(ex.tneg)[j * ex.ldtneg + i] = -c[j];
+    }
   });
 }
 

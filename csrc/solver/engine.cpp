@@ -877,9 +877,15 @@ void Engine::lookahead_update(int64_t u) {
     dev_.wait(ms, ev_la_[par]);
     const int pe = prof_begin(ms);
     if (rows > 0) {
+      // the first column block's new multipliers -X[:, x0:x0+m]^T go straight into segment 0 of
+      // the next panel's multiplier panel (GemmExtra::tneg, no separate extract launch; neutral to
+      // -1 % in the A/B of profiles/side_chain_r3.md, one launch fewer per panel)
+      GemmExtra ex = prows;
+      ex.tneg = At_[(u + 1) % 3];
+      ex.ldtneg = rows;
+      ex.tneg_cols = m;
       dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, x1 - x0, K, At_[u % 3], rows, LA_[par],
-                x1 - x0, elem(X_, x0), npad, ms, prows);
-      dev_.extract_neg_t(opt_.dtype, At_[(u + 1) % 3], rows, X_, npad, rows, x0, m, ms);
+                x1 - x0, elem(X_, x0), npad, ms, ex);
     }
     prof_end(PH_UPDATE, pe, ms);
     dev_.record(ev_L_, ms);

@@ -42,19 +42,20 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, op: str = "acc", a_k
     """C += A@B (op="acc") or C = A@B (op="store").  With a_kmajor, ``A`` is given as A^T (K x M).
 
     Elimination extras (op="acc"): C enters as 0 in the columns ``zero_cols`` = (c0, c1) and in the
-    row blocks [r, r + zero_row_height) for r in ``zero_rows`` (at most 8).  ``tneg`` (N x M view,
-    unit column stride): also receives -C^T, the multiplier panel the engine's column update
-    writes as it stores C.  ``latency``: the small-tile launch the pivot chain uses."""
+    row blocks [r, r + zero_row_height) for r in ``zero_rows`` (at most 8).  ``tneg`` (Nt x M view,
+    Nt <= N, unit column stride): also receives -C^T of C's first Nt columns, the multiplier panel
+    the engine's column / look-ahead updates write as they store C.  ``latency``: the small-tile
+    launch the pivot chain uses."""
     assert A.dtype == B.dtype == C.dtype and A.stride(-1) == 1 and B.stride(-1) == 1 and C.stride(-1) == 1
     M, N = C.shape
     K = A.shape[0] if a_kmajor else A.shape[1]
-    tp, ldt = 0, 0
+    tp, ldt, tcols = 0, 0, 0
     if tneg is not None:
-        assert tneg.dtype == C.dtype and tneg.shape == (N, M) and tneg.stride(-1) == 1
-        tp, ldt = _p(tneg), tneg.stride(0)
+        assert tneg.dtype == C.dtype and tneg.shape[1] == M and 0 < tneg.shape[0] <= N and tneg.stride(-1) == 1
+        tp, ldt, tcols = _p(tneg), tneg.stride(0), tneg.shape[0]
     device_for(C).gemm(_DT[C.dtype], op, a_kmajor, M, N, K, _p(A), A.stride(0), _p(B), B.stride(0), _p(C), C.stride(0),
                        int(zero_cols[0]), int(zero_cols[1]), [int(r) for r in zero_rows], int(zero_row_height),
-                       tp, ldt, bool(latency))
+                       tp, ldt, bool(latency), tcols)
     return C
 
 

@@ -54,26 +54,33 @@ def test_generate_matches_numpy():
 
 
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
-@pytest.mark.parametrize("M,K,latency,variant", [(300, 256, True, "auto"), (4096, 384, True, "auto"),
-                                                 (1000, 512, False, "auto"), (777, 128, False, "glds"),
-                                                 (2048, 256, False, "big"), (513, 128, True, "narrow")])
-def test_gemm_tneg_epilogue(native, dtype, M, K, latency, variant):
-    """Column update with the fused multiplier write: C += A B and tneg = -C^T (bit-identical)."""
+@pytest.mark.parametrize("M,K,latency,variant,N,tcols", [(300, 256, True, "auto", 128, 128),
+                                                          (4096, 384, True, "auto", 128, 128),
+                                                          (1000, 512, False, "auto", 128, 128),
+                                                          (777, 128, False, "glds", 128, 128),
+                                                          (2048, 256, False, "big", 128, 128),
+                                                          (513, 128, True, "narrow", 128, 128),
+                                                          (1000, 256, False, "glds", 512, 128),
+                                                          (16384, 512, False, "auto", 512, 128),
+                                                          (1030, 256, False, "narrow", 384, 100)])
+def test_gemm_tneg_epilogue(native, dtype, M, K, latency, variant, N, tcols):
+    """Column / look-ahead update with the fused multiplier write: C += A B and tneg = -C^T of the
+    first tcols columns (bit-identical to C), on every tile family incl. the LDS-DMA kernel."""
     native.set_gemm_variant(variant)
     try:
-        N = 128
         At = _rand((K, M), dtype, 21).cuda()
         B = _rand((K, N), dtype, 22).cuda()
         C = _rand((M, N), dtype, 23)
         ref = C.double() + At.cpu().double().t() @ B.cpu().double()
         Cd = C.cuda()
         T = torch.full((N, M + 8), 7.0, dtype=dtype, device="cuda")
-        ops.gemm(At, B, Cd, op="acc", a_kmajor=True, tneg=T[:, :M],
+        ops.gemm(At, B, Cd, op="acc", a_kmajor=True, tneg=T[:tcols, :M],
                  latency=latency)
         tol = (1e-12 if dtype == torch.float64 else 2e-5) * K
         assert (Cd.cpu().double() - ref).abs().max().item() < tol
-        assert torch.equal(T[:, :M].cpu(), -Cd.cpu().t())
-        assert torch.equal(T[:, M:].cpu(), torch.full((N, 8), 7.0, dtype=dtype))
+        assert torch.equal(T[:tcols, :M].cpu(), -Cd.cpu().t()[:tcols])
+        assert torch.equal(T[:tcols, M:].cpu(), torch.full((tcols, 8), 7.0, dtype=dtype))
+        assert torch.equal(T[tcols:].cpu(), torch.full((N - tcols, M + 8), 7.0, dtype=dtype))
     finally:
         native.set_gemm_variant("auto")
 

@@ -168,6 +168,10 @@ def test_host_gemm_tneg_epilogue():
     assert (C - ref).abs().max().item() < 1e-12
     assert torch.equal(T[:, :90], -C.t())
     assert torch.equal(T[:, 90:], torch.full((70, 6), 3.0, dtype=torch.float64))
+    T2 = torch.full((70, 90), 5.0, dtype=torch.float64)
+    C2 = torch.rand(90, 70, generator=g, dtype=torch.float64)
+    ops.gemm(A.t().contiguous(), B, C2, op="acc", a_kmajor=True, tneg=T2[:30])
+    assert torch.equal(T2[:30], -C2.t()[:30]) and torch.equal(T2[30:], torch.full((40, 90), 5.0, dtype=torch.float64))
 
 
 def test_python_solve_vector_native_path(native):
