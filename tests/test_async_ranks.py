@@ -32,6 +32,18 @@ def test_async_ranks_match_numpy(p, depth):
     assert rep["device"].startswith("host-async")
 
 
+@pytest.mark.parametrize("depth", [2, 4])
+def test_async_ranks_odd_chunk_tail(depth):
+    """The chunk plan of n = 8192, m = 60 at p = 8 in miniature: 137 block rows, auto chunks of 68
+    blocks and a one-block last chunk and panel (profiles/depth_pgt1.md, the depth-2 ordering item),
+    jittered asynchronous ranks."""
+    n, m = 137 * 8, 8
+    A = generate_matrix(n, "random", 5)[::-1].copy()
+    rep = _inv(A, m, 8, depth, jitter=300.0)
+    ref = np.linalg.inv(A)
+    assert np.abs(rep["inverse"] - ref).max() / np.abs(ref).max() < 1e-8
+
+
 @pytest.mark.parametrize("p", [2, 4])
 def test_async_equals_synchronous_loopback_bitwise(p):
     # same kernels, same operand order: the asynchronous schedule may only change timing
