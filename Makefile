@@ -22,7 +22,7 @@ LDLIBS    := -L$(ROCM)/lib -lrccl -lamdhip64 -lrocprofiler-sdk-roctx -lpthread
 KERNELS   := gemm blockinv blockinv_mfma blockinv_big misc
 HOST_SRC  := solver/engine solver/runner runtime/host_device runtime/hip_device \
              runtime/loopback_comm runtime/async_loopback_comm runtime/async_host_device \
-             runtime/shadow_comm runtime/rccl_comm runtime/comm io/matrix_io
+             runtime/shadow_comm runtime/rccl_comm runtime/comm runtime/race_check io/matrix_io
 
 KOBJ      := $(patsubst %,$(BUILD)/kernels/%.o,$(KERNELS))
 HOBJ      := $(patsubst %,$(BUILD)/%.o,$(HOST_SRC))

@@ -35,6 +35,10 @@
 //   --bcast auto|ring|direct  pivot-row broadcast algorithm at p > 2 (sets GJ_BCAST; auto = timed
 //                        against each other at startup, Comm::tune_bcast)
 //   --sync-debug         synchronise after every phase (race screening)
+//   --race-check         run under the happens-before schedule checker (RaceCheckDevice): every
+//                        unordered conflicting access is printed to stderr and the exit code is 2
+//   --check-residual TOL exit 2 (after the normal output) when the residual is not finite or
+//                        exceeds TOL: a wrong inverse is a failure, not a slow success
 //   --profile            per-phase device timers (in --json) + roctx ranges for rocprofv3
 //   --comm-timeout S     seconds a rank waits for a pivot before declaring a peer failure
 //   --wait-debugger S    sleep S seconds at start (reference -DSLEEP, main.cpp:8, :70-72)
@@ -111,6 +115,7 @@ int main(int argc, char* argv[]) {
   bool json = false;
   std::string device = "auto", out_file, x_file;
   int wait_dbg = 0;
+  double check_tol = -1.0;  // --check-residual
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     auto val = [&](const char* name) -> const char* {
@@ -167,6 +172,8 @@ int main(int argc, char* argv[]) {
         setenv("GJ_BCAST", b.c_str(), 1);
       }
       else if (a == "--sync-debug") cfg.solve.sync_debug = true;
+      else if (a == "--race-check") cfg.race_check = true;
+      else if (a == "--check-residual") check_tol = std::atof(val("--check-residual"));
       else if (a == "--profile") cfg.solve.profile = true;
       else if (a == "--comm-timeout") cfg.solve.comm_timeout_s = std::atof(val("--comm-timeout"));
       else if (a == "--wait-debugger") wait_dbg = std::atoi(val("--wait-debugger"));
@@ -239,5 +246,21 @@ int main(int argc, char* argv[]) {
   if (!out_file.empty()) write_matrix_file(out_file, n, rep.inverse.data(), n);
   if (!x_file.empty()) write_vector_file(x_file, n, rep.x.data());
   if (json) json_report(cfg, rep);
-  return 0;
+  int rc = 0;
+  if (cfg.race_check) {
+    for (const auto& r : rep.races) std::fprintf(stderr, "race: %s\n", r.c_str());
+    std::fprintf(stderr, "race check: %lld unordered conflicting accesses in %lld ops\n",
+                 (long long)rep.race_count, (long long)rep.race_ops);
+    if (rep.race_count > 0) rc = 2;
+  }
+  if (check_tol >= 0.0) {
+    if (!rep.residual_computed) {
+      std::fprintf(stderr, "residual check: no residual computed (--residual never / compat at p == 1)\n");
+      rc = 2;
+    } else if (!std::isfinite(rep.residual) || rep.residual > check_tol) {
+      std::fprintf(stderr, "residual check failed: residual %e exceeds %e\n", rep.residual, check_tol);
+      rc = 2;
+    }
+  }
+  return rc;
 }

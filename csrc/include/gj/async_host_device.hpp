@@ -67,6 +67,9 @@ class AsyncHostDevice : public Device {
   void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                      int32_t* valid, const int32_t* used, const Layout& L, double thresh,
                      int s) override;
+  bool block_inverse_select(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
+                            int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                            const PivotSelectArgs& sel, int s) override;
   void candidate_maxabs(DType dt, const void* Lt, int64_t ldl, double* scores, int32_t* valid,
                         const int32_t* used, const Layout& L, double thresh, int s) override;
   void gather_candidate(DType dt, void* sel, const void* Lt, int64_t ldl, const PivotRec* rec, const Layout& L,
@@ -124,6 +127,9 @@ class AsyncHostDevice : public Device {
   void fail(std::exception_ptr e);
   void rethrow();
   void check_stream(int s) const;
+  // pivot_global's work on the worker thread (the pinned host record's step field written last)
+  void pivot_global_now(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos, int32_t* phys_at, int32_t* used,
+                        int32_t* seq, PivotResult* out, PivotResult* host_out, int s);
 
   HostDevice inner_;
   double jitter_us_, wait_timeout_s_;

@@ -102,8 +102,10 @@ class LoopbackComm : public Comm {
   // size, root, stream role) at the same point of its program, as RCCL requires; a divergence
   // throws on every rank instead of silently exchanging the wrong buffers.
   void enter(const std::string& signature);
+  void meet(Device& dev);
   std::shared_ptr<LoopbackHub> hub_;
   int r_;
+  uint64_t meets_ = 0;
 };
 
 // ---------------------------------------------------------------- asynchronous virtual ranks
@@ -143,6 +145,7 @@ class AsyncLoopbackComm : public Comm {
   int r_;
   double jitter_us_;
   uint64_t rng_;
+  bool drop_root_wait_ = false;  // GJ_TEST_DROP_WAIT=bcast_root (tests)
 };
 
 }  // namespace gj

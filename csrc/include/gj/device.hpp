@@ -119,6 +119,21 @@ class Device {
   // Returns the number of CUs actually reserved.  Call while the device is idle.
   virtual int reserve_cus(int n) { (void)n; return 0; }
 
+  // ---- schedule-checking hooks (RaceCheckDevice, gj/race_check.hpp; no-ops elsewhere) ----
+  // Where the caller is (read at every op for reports): its step counter and phase name.
+  virtual void trace_context(const int64_t* step, const char* const* phase) { (void)step; (void)phase; }
+  // Name of an allocation in reports.
+  virtual void label(const void* p, const char* name) { (void)p; (void)name; }
+  // The host thread reads / writes host-visible memory directly (pinned staging, polled records).
+  virtual void host_access(const void* p, size_t bytes, bool write) { (void)p; (void)bytes; (void)write; }
+  // The host observed the record at p that a device op published (pivot_global's host_out): it
+  // now knows everything that op was ordered after.
+  virtual void host_acquire(const void* p, size_t bytes) { (void)p; (void)bytes; }
+  // Host-thread ordering across devices (LoopbackComm's rendezvous): a handle of everything this
+  // device's host has observed, and joining a peer's handle into it.
+  virtual std::shared_ptr<void> host_mark() { return nullptr; }
+  virtual void host_wait_mark(const std::shared_ptr<void>& h) { (void)h; }
+
   // ---- kernels ----
   // X (layout.rows x npad, ld npad) := A' restricted to this rank's block rows.
   virtual void generate(DType dt, void* X, const Layout& L, GenSpec g, int s) = 0;

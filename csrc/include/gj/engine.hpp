@@ -49,7 +49,7 @@ struct SolveOptions {
   DType dtype = DType::F64;
   int64_t chunk_cols = 0;   // pipelining granularity of the pivot-row broadcast (0 = auto)
   int depth = 0;            // elimination steps fused per trailing update (K = depth*m), 1..8;
-                            // 0 = auto: 2 up to N = 8192 (pivot-chain-bound); 8 on ranks of
+                            // 0 = auto: 2 up to N = 8192 on one rank (pivot-chain-bound); 8 on ranks of
                             // <= 4096 rows of a p > 1 job with N > 16384 (p = 8 at N = 32768);
                             // else 4 (profiles/small_n_sweep.md, profiles/depth_pgt1.md)
   double eps = kDefaultEps;
@@ -174,6 +174,7 @@ class Engine {
   int alloc_buffers(std::string& why);
   void alloc_work(int64_t wmax);
   void free_work();     // everything but the matrix panels
+  void label_work();    // buffer names for schedule-check reports
   void free_buffers();
   // Pivot search for step t on the multiplier segment Lt (SIDE stream); result -> piv_host_[t&1].
   void select(int64_t t, const void* Lt, bool full = false);
@@ -295,6 +296,14 @@ class Engine {
   int64_t cur_step_ = -1;
   const char* cur_phase_ = "setup";
   int64_t hang_step_ = -1;  // GJ_TEST_HANG (fault injection)
+  // GJ_TEST_DROP_WAIT=<name>[,<name>]: leave out one ordering edge of the schedule (a planted
+  // hazard the happens-before checker must report; tests only): "cp" the SIDE wait for the chunk
+  // pass two panels back, "edit" MAIN's wait for the owner edits, "b" MAIN's wait for a chunk's
+  // broadcast, "x" the chunk pass's exclusion of the next panel's columns
+  std::string drop_wait_;
+  bool dropped(const char* name) const {
+    return !drop_wait_.empty() && drop_wait_.find(std::string(",") + name + ",") != std::string::npos;
+  }
 };
 
 }  // namespace gj

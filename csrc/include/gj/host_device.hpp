@@ -45,6 +45,9 @@ class HostDevice : public Device {
   void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                      int32_t* valid, const int32_t* used, const Layout& L, double thresh,
                      int s) override;
+  bool block_inverse_select(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
+                            int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                            const PivotSelectArgs& sel, int s) override;
   void candidate_maxabs(DType dt, const void* Lt, int64_t ldl, double* scores, int32_t* valid,
                         const int32_t* used, const Layout& L, double thresh, int s) override;
   void gather_candidate(DType dt, void* sel, const void* Lt, int64_t ldl, const PivotRec* rec, const Layout& L,

@@ -38,6 +38,9 @@ struct RunConfig {
   // steps (-1 = auto: 10 for fp32 solves, 2 for fp64), stop at backward error <= refine_tol
   int refine = -1;
   double refine_tol = 1e-15;
+  // Run every rank's device under the happens-before schedule checker (RaceCheckDevice, one
+  // checker shared by the rank threads); reports land in RunReport::races.
+  bool race_check = false;
 };
 
 struct RunReport {
@@ -63,6 +66,11 @@ struct RunReport {
   double rhs_seconds = 0;           // x = inv(A) b (GEMV + all-gather), max over ranks
   std::vector<double> x_head;       // first min(n, print_max) entries of x
   std::vector<double> x;            // n entries if keep_solution
+  // race_check: unordered conflicting accesses found (total, the first distinct ones described),
+  // ops checked
+  int64_t race_count = 0;
+  std::vector<std::string> races;
+  int64_t race_ops = 0;
 };
 
 RunReport run_local(const RunConfig& cfg);

@@ -18,6 +18,7 @@
 #include "gj/hip_device.hpp"
 #include "gj/host_device.hpp"
 #include "gj/io.hpp"
+#include "gj/race_check.hpp"
 #include "gj/runner.hpp"
 #include "../kernels/kernels.hpp"
 
@@ -543,6 +544,18 @@ PYBIND11_MODULE(_C, mod) {
         return e.eng->residual_rows(p, n);
       });
 
+  // geometry of the schedule checker (tests): regions as (base, pitch, width, height) in bytes
+  auto region = [](py::tuple t) {
+    MemRegion r;
+    r.base = reinterpret_cast<const char*>((uintptr_t)t[0].cast<int64_t>());
+    r.pitch = t[1].cast<int64_t>();
+    r.width = t[2].cast<int64_t>();
+    r.height = t[3].cast<int64_t>();
+    return r;
+  };
+  mod.def("_regions_overlap", [region](py::tuple a, py::tuple b) { return regions_overlap(region(a), region(b)); });
+  mod.def("_region_covers", [region](py::tuple a, py::tuple b) { return region_covers(region(a), region(b)); });
+
   mod.def("run_local", [](py::dict d) {
     RunConfig c;
     c.n = d["n"].cast<int64_t>();
@@ -574,6 +587,7 @@ PYBIND11_MODULE(_C, mod) {
     if (d.contains("repeats")) c.repeats = d["repeats"].cast<int>();
     if (d.contains("refine")) c.refine = d["refine"].cast<int>();
     if (d.contains("refine_tol")) c.refine_tol = d["refine_tol"].cast<double>();
+    if (d.contains("race_check")) c.race_check = d["race_check"].cast<bool>();
     py::array_t<double, py::array::c_style | py::array::forcecast> inp;
     if (d.contains("input") && !d["input"].is_none()) {
       inp = d["input"].cast<py::array_t<double, py::array::c_style | py::array::forcecast>>();
@@ -608,6 +622,11 @@ PYBIND11_MODULE(_C, mod) {
     o["device"] = r.device_desc;
     o["comm"] = r.comm_desc;
     o["gflops_nominal"] = r.gflops_nominal;
+    if (c.race_check) {
+      o["race_count"] = r.race_count;
+      o["races"] = r.races;
+      o["race_ops"] = r.race_ops;
+    }
     if (r.rhs_solved) {
       o["axb_residual"] = r.rhs_residual;
       o["axb_seconds"] = r.rhs_seconds;

@@ -240,6 +240,18 @@ void AsyncHostDevice::block_inverse(DType dt, const void* Lt, int64_t ldl, void*
                                     double thresh, int s) {
   enqueue(s, [=] { inner_.block_inverse(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, s); });
 }
+bool AsyncHostDevice::block_inverse_select(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
+                                           int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                                           const PivotSelectArgs& sel, int s) {
+  if (L.m <= 16 || L.m > 128 || L.nblk <= 0) return false;  // = HostDevice's range
+  enqueue(s, [=] {
+    inner_.block_inverse(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, s);
+    inner_.pivot_local(scores, valid, used, sel.pos, L, sel.rec, s);
+    if (sel.single) pivot_global_now(sel.rec, 1, sel.t, sel.pos_w, sel.phys_at, sel.used_w, sel.seq, sel.out,
+                                     sel.host_out, s);
+  });
+  return true;
+}
 void AsyncHostDevice::candidate_maxabs(DType dt, const void* Lt, int64_t ldl, double* scores, int32_t* valid,
                                        const int32_t* used, const Layout& L, double thresh, int s) {
   enqueue(s, [=] { inner_.candidate_maxabs(dt, Lt, ldl, scores, valid, used, L, thresh, s); });
@@ -261,17 +273,20 @@ void AsyncHostDevice::pivot_local(const double* scores, const int32_t* valid, co
 void AsyncHostDevice::pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos,
                                    int32_t* phys_at, int32_t* used, int32_t* seq, PivotResult* out,
                                    PivotResult* host_out, int s) {
-  enqueue(s, [=] {
-    inner_.pivot_global(recs, p, t, pos, phys_at, used, seq, out, nullptr, s);
-    if (host_out) {
-      PivotResult r = *out;
-      const int32_t step = r.step;
-      r.step = -1;
-      std::memcpy(static_cast<void*>(host_out), &r, sizeof(r));
-      std::atomic_thread_fence(std::memory_order_release);
-      *reinterpret_cast<volatile int32_t*>(&host_out->step) = step;
-    }
-  });
+  enqueue(s, [=] { pivot_global_now(recs, p, t, pos, phys_at, used, seq, out, host_out, s); });
+}
+void AsyncHostDevice::pivot_global_now(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos, int32_t* phys_at,
+                                       int32_t* used, int32_t* seq, PivotResult* out, PivotResult* host_out,
+                                       int s) {
+  inner_.pivot_global(recs, p, t, pos, phys_at, used, seq, out, nullptr, s);
+  if (host_out) {
+    PivotResult r = *out;
+    const int32_t step = r.step;
+    r.step = -1;
+    std::memcpy(static_cast<void*>(host_out), &r, sizeof(r));
+    std::atomic_thread_fence(std::memory_order_release);
+    *reinterpret_cast<volatile int32_t*>(&host_out->step) = step;
+  }
 }
 void AsyncHostDevice::owner_edits(DType dt, void* At, int64_t ldl, int64_t row0, int64_t j, int64_t m,
                                   void* lrow, void* ht, const void* inv_blk, int s) {

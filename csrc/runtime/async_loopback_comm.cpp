@@ -6,6 +6,7 @@
 // once the collective is complete for that rank.  No host thread ever waits for a stream here.
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -28,7 +29,12 @@ std::string sig(const char* kind, size_t bytes, int root, int s) {
 
 AsyncLoopbackComm::AsyncLoopbackComm(std::shared_ptr<LoopbackHub> hub, int rank, double jitter_us,
                                      uint64_t seed)
-    : hub_(std::move(hub)), r_(rank), jitter_us_(jitter_us), rng_(seed * 1000003ull + (uint64_t)rank + 1) {}
+    : hub_(std::move(hub)), r_(rank), jitter_us_(jitter_us), rng_(seed * 1000003ull + (uint64_t)rank + 1) {
+  // GJ_TEST_DROP_WAIT=bcast_root: broadcast receivers copy without waiting for the root's marker (a
+  // planted cross-rank hazard for the schedule checker's tests)
+  if (const char* e = std::getenv("GJ_TEST_DROP_WAIT"))
+    drop_root_wait_ = (std::string(",") + e + ",").find(",bcast_root,") != std::string::npos;
+}
 
 std::string AsyncLoopbackComm::describe() const {
   return "async-loopback(" + std::to_string(size()) +
@@ -65,7 +71,7 @@ void AsyncLoopbackComm::bcast(Device& dev, void* buf, size_t bytes, int root, in
   jitter(dev, s);
   enter(sig("bcast", bytes, root, s), buf, dev.mark(s));
   if (r_ != root) {
-    dev.wait_mark(s, hub_->mk[root]);
+    if (!drop_root_wait_) dev.wait_mark(s, hub_->mk[root]);
     dev.copy(buf, hub_->ptr[root], bytes, s);
     hub_->done[r_] = dev.mark(s);
   }

@@ -47,6 +47,19 @@ void LoopbackComm::enter(const std::string& signature) {
                                          hub_->sig[q] + " while rank 0 entered " + hub_->sig[0]);
 }
 
+// Rendezvous that also carries the host threads' ordering (Device::host_mark): after it, every
+// rank's host has observed what every peer's host had observed when it arrived (the streams each
+// drained before).  Only the schedule checker (RaceCheckDevice) looks at the marks.
+// Consecutive meets alternate between two slot vectors: a rank writes its slot of meet k + 2 only
+// after the rendezvous of meet k + 1, which every rank reaches only once it has read meet k's.
+void LoopbackComm::meet(Device& dev) {
+  auto& slot = (meets_++ & 1) ? hub_->done : hub_->mk;
+  slot[r_] = dev.host_mark();
+  hub_->arrive_and_wait();
+  for (int q = 0; q < size(); ++q)
+    if (q != r_) dev.host_wait_mark(slot[q]);
+}
+
 static std::string sig(const char* kind, size_t bytes, int root, int s) {
   return std::string(kind) + "(" + std::to_string(bytes) + " B, root " + std::to_string(root) +
          ", stream " + std::to_string(s) + ")";
@@ -56,21 +69,21 @@ void LoopbackComm::allgather(Device& dev, const void* send, void* recv, size_t b
   dev.sync_stream(s);
   enter(sig("allgather", bytes, -1, s));
   hub_->ptr[r_] = send;
-  hub_->arrive_and_wait();
+  meet(dev);
   for (int q = 0; q < size(); ++q)
     dev.copy(static_cast<char*>(recv) + (size_t)q * bytes, hub_->ptr[q], bytes, s);
   dev.sync_stream(s);
-  hub_->arrive_and_wait();
+  meet(dev);
 }
 
 void LoopbackComm::bcast(Device& dev, void* buf, size_t bytes, int root, int s) {
   dev.sync_stream(s);
   enter(sig("bcast", bytes, root, s));
   hub_->ptr[r_] = buf;
-  hub_->arrive_and_wait();
+  meet(dev);
   if (r_ != root) dev.copy(buf, hub_->ptr[root], bytes, s);
   dev.sync_stream(s);
-  hub_->arrive_and_wait();
+  meet(dev);
 }
 
 void LoopbackComm::allreduce_max(Device& dev, double* buf, size_t count, int s) {
@@ -97,7 +110,7 @@ void LoopbackComm::group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) 
   mine.clear();
   for (const auto& op : ops)
     if (op.send) mine.push_back(op);
-  hub_->arrive_and_wait();
+  meet(dev);
   // receives from peer q match q's sends to me in issue order (NCCL p2p semantics)
   std::vector<size_t> cursor(size(), 0);
   for (const auto& op : ops) {
@@ -111,12 +124,12 @@ void LoopbackComm::group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) 
     ++c;
   }
   dev.sync_stream(s);
-  hub_->arrive_and_wait();
+  meet(dev);
 }
 
 void LoopbackComm::barrier(Device& dev) {
   dev.sync_all();
-  hub_->arrive_and_wait();
+  meet(dev);
 }
 
 double LoopbackComm::host_max(Device&, double v) {

@@ -90,7 +90,12 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // communication-cost model 0.167 vs 0.177 s, while depth 6 / 8 lose at p = 1 / 2 / 4 and at
   // N = 16384: profiles/depth_pgt1.md)
   const bool small_rank = L_.p > 1 && L_.max_nblk * L_.m <= 4096;
-  const int want = opt_.depth > 0 ? opt_.depth : (L_.npad <= 8192 ? 2 : (small_rank && L_.npad > 16384) ? 8 : 4);
+  // Depth 2 stays with one rank: one async-virtual-rank GPU run at p = 8, depth 2 returned a wrong
+  // inverse (profiles/depth_pgt1.md) that the happens-before checker (race_check.hpp) does not
+  // explain -- the schedule matrix of tests/test_race_check.py is race-free -- so p > 1 keeps the
+  // depth the multi-rank tests and the scaling runs have always used.
+  const int want = opt_.depth > 0 ? opt_.depth
+                                  : (L_.p == 1 && L_.npad <= 8192) ? 2 : (small_rank && L_.npad > 16384) ? 8 : 4;
   d_ = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)want, (int64_t)kMaxDepth, L_.Nr}));
 
   // Column chunk plan: fixed partition of the Nr block columns into runs of a multiple of d blocks.
@@ -142,6 +147,8 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
 
   comm_.set_timeout(opt_.comm_timeout_s);
   hang_step_ = injected_hang_step(L_.k);
+  if (const char* e = std::getenv("GJ_TEST_DROP_WAIT")) drop_wait_ = std::string(",") + e + ",";
+  dev_.trace_context(&cur_step_, &cur_phase_);  // names the step / phase in schedule-check reports
   // Allocation, agreed on every rank BEFORE any other collective (reference main.cpp:366-381 and
   // :428-436): 2 = this rank's matrix panels do not fit ("Not enough memory!", thrown on every
   // rank), 1 = the elimination work space does not ("not enough memory for block", reported by
@@ -180,7 +187,10 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
 
 }
 
-Engine::~Engine() { free_buffers(); }
+Engine::~Engine() {
+  free_buffers();
+  dev_.trace_context(nullptr, nullptr);
+}
 
 Engine::Policy Engine::policy() const {
   Policy p;
@@ -222,6 +232,8 @@ int Engine::alloc_buffers(std::string& why) {
                                         std::to_string(need_matrix) + " bytes, have " + std::to_string(avail));
     X_ = dev_.alloc(panel);
     out_ = dev_.alloc(panel);
+    dev_.label(X_, "X");
+    dev_.label(out_, "out");
   } catch (const Error& e) {
     if (e.status() != Status::NoMemory) throw;
     why = e.what();
@@ -292,6 +304,7 @@ void Engine::alloc_work(int64_t wmax) {
   piv_host_ = static_cast<PivotResult*>(dev_.alloc_pinned_coherent(sizeof(PivotResult) * 2));
   ihost_ = static_cast<int32_t*>(dev_.alloc_pinned(sizeof(int32_t) * ihost_len_));
   dhost_ = static_cast<double*>(dev_.alloc_pinned(sizeof(double) * 64));
+  label_work();
 
   if (ev_L_ >= 0) return;  // events are the device's; created once
   ev_L_ = dev_.create_event();
@@ -305,6 +318,31 @@ void Engine::alloc_work(int64_t wmax) {
     for (size_t c = 0; c < cb0_.size(); ++c) ev_b_[i].push_back(dev_.create_event());
   }
   for (size_t c = 0; c < cb0_.size(); ++c) ev_c_.push_back(dev_.create_event());
+}
+
+// Buffer names in schedule-check reports (RaceCheckDevice).
+void Engine::label_work() {
+  static const char* at[3] = {"At[0]", "At[1]", "At[2]"};
+  static const char* rb[2] = {"Rb[0]", "Rb[1]"};
+  static const char* pp[2] = {"PP[0]", "PP[1]"};
+  static const char* la[2] = {"LA[0]", "LA[1]"};
+  for (int i = 0; i < 3; ++i) dev_.label(At_[i], at[i]);
+  for (int i = 0; i < 2; ++i) {
+    dev_.label(Rb_[i], rb[i]);
+    dev_.label(PP_[i], pp[i]);
+    dev_.label(LA_[i], la[i]);
+    for (int j = 0; j < d_; ++j) {
+      dev_.label(Lrow_[i][j], (std::string("Lrow[") + char('0' + i) + "][" + char('0' + j) + "]").c_str());
+      dev_.label(Ht_[i][j], (std::string("Ht[") + char('0' + i) + "][" + char('0' + j) + "]").c_str());
+    }
+  }
+  const std::pair<const void*, const char*> named[] = {
+      {T_, "T"}, {RP_, "RP"}, {T2_, "T2"}, {inv_, "inv"}, {sel_, "sel"}, {inv1_, "inv1"}, {scores_, "scores"},
+      {valid_, "valid"}, {pos_, "pos"}, {phys_at_, "phys_at"}, {used_, "used"}, {seq_, "seq"}, {myrec_, "myrec"},
+      {sel_done_, "sel_done"}, {recs_, "recs"}, {piv_dev_, "piv_dev"}, {dscratch_, "dscratch"},
+      {iscratch_, "iscratch"}, {piv_host_, "piv_host"}, {ihost_, "ihost"}, {dhost_, "dhost"}};
+  for (const auto& nv : named)
+    if (nv.first) dev_.label(nv.first, nv.second);
 }
 
 void Engine::free_work() {
@@ -385,6 +423,7 @@ void Engine::wait_pivot(int par, int64_t step, double& host_wait) {
     }
   }
   std::atomic_thread_fence(std::memory_order_acquire);
+  dev_.host_acquire(&piv_host_[par], sizeof(PivotResult));
   host_wait += now_s() - w0;
 }
 
@@ -525,7 +564,10 @@ void Engine::select(int64_t t, const void* Lt, bool full) {
     // supports it (one launch fewer on the pivot chain per step); otherwise as its own launch.
     // One rank: the local record is the gathered set -> local argmin + book-keeping in one go; the
     // result goes straight to pinned host memory (no copy kernel), the host polls its step field.
-    if (L_.p == 1) piv_host_[par].step = -1;
+    if (L_.p == 1) {
+      dev_.host_access(&piv_host_[par].step, sizeof(int32_t), true);
+      piv_host_[par].step = -1;
+    }
     bool fused = false;
     if (L_.nblk > 0) {
       dev_.set_block_inverse_hint(bi_hint_);  // per call: a device may be shared with other users
@@ -561,11 +603,13 @@ void Engine::select(int64_t t, const void* Lt, bool full) {
     prof_end(PH_PIVOT, pe, S_SIDE);
   }
   if (hang_step_ == t) {  // GJ_TEST_HANG: this rank never joins the exchange of step t
+    dev_.host_access(&piv_host_[par].step, sizeof(int32_t), true);
     piv_host_[par].step = -1;
     return;
   }
   pe = prof_begin(S_SIDE);
   if (L_.p > 1) comm_.allgather(dev_, myrec_, recs_, sizeof(PivotRec), S_SIDE);
+  dev_.host_access(&piv_host_[par].step, sizeof(int32_t), true);
   piv_host_[par].step = -1;
   dev_.pivot_global(L_.p > 1 ? recs_ : myrec_, (int32_t)L_.p, (int32_t)t, pos_, phys_at_, used_, seq_, piv_dev_,
                     &piv_host_[par], S_SIDE);
@@ -591,7 +635,7 @@ void Engine::begin_panel(int64_t v) {
   // this panel's steps rewrite Lrow_ / Ht_ / PP_[v & 1], which the COMM chunk pass of panel v - 2
   // reads (with the look-ahead update on SIDE nothing else orders the two; the asynchronous
   // virtual-rank test, tests/test_async_ranks.py, fails without this wait)
-  if (v >= 2) dev_.wait(S_SIDE, ev_cp_[v & 1]);
+  if (v >= 2 && !dropped("cp")) dev_.wait(S_SIDE, ev_cp_[v & 1]);
   select(panel_t0(v), At_[v % 3]);
 }
 
@@ -782,19 +826,31 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
   const bool has_next = (v + 1 < npanels());
   const int64_t start = has_next ? chunk_of_[panel_t0(v + 1)] : 0;
   const int64_t pc0 = t0 * m, pc1 = (t0 + q) * m;  // panel columns
+  const int64_t xn0 = has_next ? panel_t0(v + 1) * m : 0;  // the next panel's columns
+  const int64_t xn1 = has_next ? (panel_t0(v + 1) + panel_q(v + 1)) * m : 0;
   dev_.wait(S_COMM, ev_pp_[par][q - 1]);  // all panel pieces, multiplier rows and H_t (SIDE)
   cur_phase_ = "pivot-row broadcast";
   for (int64_t i = 0; i < C; ++i) {
     const int64_t c = (start + i) % C;
     const int64_t c0 = cb0_[c] * m, c1 = cb1_[c] * m, W = c1 - c0;
     if (wait_main) dev_.wait(S_COMM, ev_c_[c]);
-    int64_t ra[2], rb[2], nr = 0;
+    // the chunk's columns minus the panel's own (they come from the panel pieces) and minus the next
+    // panel's (the look-ahead rows carried them, MAIN's chunk pass skips them, and the look-ahead
+    // update on SIDE rewrites X there while this pass runs: reading them would race it)
+    int64_t ra[3], rb[3], nr = 0;
     const bool has_panel = (pc0 >= c0 && pc0 < c1);
-    if (has_panel) {
-      if (pc0 > c0) { ra[nr] = c0; rb[nr] = pc0; ++nr; }
-      if (c1 > pc1) { ra[nr] = pc1; rb[nr] = c1; ++nr; }
-    } else {
-      ra[0] = c0; rb[0] = c1; nr = 1;
+    {
+      int64_t cut0[2], cut1[2], ncut = 0;
+      if (has_panel) { cut0[ncut] = pc0; cut1[ncut++] = pc1; }
+      if (has_next && !dropped("x")) { cut0[ncut] = xn0; cut1[ncut++] = xn1; }
+      int64_t a = c0;
+      for (int64_t z = 0; z < ncut; ++z) {  // the cuts are ordered (the next panel follows this one)
+        const int64_t lo = std::max(cut0[z], c0), hi = std::min(cut1[z], c1);
+        if (lo >= hi) continue;
+        if (lo > a) { ra[nr] = a; rb[nr] = lo; ++nr; }
+        a = std::max(a, hi);
+      }
+      if (c1 > a) { ra[nr] = a; rb[nr] = c1; ++nr; }
     }
     char* chunk = rb_chunk(par, c);
     std::vector<BcastOp> bops;
@@ -865,7 +921,7 @@ void Engine::lookahead_update(int64_t u) {
   const int par = (int)(u & 1);
   const int64_t m = L_.m, rows = L_.rows, npad = L_.npad;
   const int64_t q = panel_q(u), K = q * m;
-  dev_.wait(S_MAIN, ev_edit_[par]);  // MAIN's chunk pass reads the edited multipliers
+  if (!dropped("edit")) dev_.wait(S_MAIN, ev_edit_[par]);  // MAIN's chunk pass reads the edited multipliers
   if (u + 1 < npanels()) {
     const int64_t tn = panel_t0(u + 1), qn = panel_q(u + 1);
     const int ms = S_SIDE;
@@ -912,7 +968,7 @@ void Engine::big_update(int64_t u) {
     const int64_t c = (start + i) % C;
     const int64_t c0 = cb0_[c] * m, c1 = cb1_[c] * m, W = c1 - c0;
     const int ms = S_MAIN;
-    dev_.wait(ms, ev_b_[par][c]);
+    if (!dropped("b")) dev_.wait(ms, ev_b_[par][c]);
     const int pe = prof_begin(ms);
     int64_t ra[2], rb[2], nr = 0;
     if (has_next && x0 >= c0 && x0 < c1) {
@@ -976,6 +1032,7 @@ SolveStats Engine::solve_steps() {
   }
 
   // book-keeping arrays: pos = phys_at = identity, used = 0
+  dev_.host_access(ihost_, sizeof(int32_t) * Nr, true);
   for (int64_t i = 0; i < Nr; ++i) ihost_[i] = (int32_t)i;
   dev_.copy(pos_, ihost_, sizeof(int32_t) * Nr, S_SIDE);
   dev_.copy(phys_at_, ihost_, sizeof(int32_t) * Nr, S_SIDE);
@@ -1040,6 +1097,7 @@ void Engine::finalize(const std::vector<int32_t>& seq) {
   // colsrc[c] = u with seq[u] == c ; dst_blk[b] = destination slot
   int32_t* colsrc = ihost_;
   int32_t* dstblk = ihost_ + Nr;
+  dev_.host_access(ihost_, sizeof(int32_t) * (Nr + std::max<int64_t>(L_.nblk, 1)), true);
   for (int64_t u = 0; u < Nr; ++u) colsrc[seq[u]] = (int32_t)u;
   for (int64_t b = 0; b < L_.nblk; ++b) {
     const int64_t g = L_.global_block(b);

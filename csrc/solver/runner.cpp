@@ -16,6 +16,7 @@
 #include "gj/hip_device.hpp"
 #include "gj/host_device.hpp"
 #include "gj/io.hpp"
+#include "gj/race_check.hpp"
 
 namespace gj {
 
@@ -31,7 +32,7 @@ struct Shared {
 };
 
 void rank_main(const RunConfig& cfg, int rank, Shared& sh, std::shared_ptr<LoopbackHub> hub,
-               const std::vector<std::string>& ids, bool use_rccl) {
+               const std::vector<std::string>& ids, bool use_rccl, std::shared_ptr<HbChecker> hb) {
   std::unique_ptr<Device> dev;
   std::unique_ptr<Comm> comm;
   const bool async = cfg.comm == "async";
@@ -63,6 +64,10 @@ void rank_main(const RunConfig& cfg, int rank, Shared& sh, std::shared_ptr<Loopb
       comm.reset(new AsyncLoopbackComm(hub, rank, cfg.jitter_us, cfg.gen.seed));
     else
       comm.reset(new LoopbackComm(hub, rank));
+  }
+  if (hb) {
+    GJ_REQUIRE(!use_rccl, "--race-check needs an in-process transport (loopback / async), not RCCL");
+    dev.reset(new RaceCheckDevice(std::move(dev), hb, "rank " + std::to_string(rank)));
   }
 
   // collective allocation check (reference main.cpp:366-381)
@@ -258,11 +263,12 @@ RunReport run_local(const RunConfig& cfg) {
     ids.push_back(RcclComm::unique_id());
   }
   auto hub = std::make_shared<LoopbackHub>(cfg.ranks);
+  std::shared_ptr<HbChecker> hb = cfg.race_check ? std::make_shared<HbChecker>() : nullptr;
   // A rank that throws (a transport error, a timed-out wait, a failed launch) reports it and
   // poisons the hub, so its peers leave their next rendezvous with an error instead of hanging.
   auto guarded = [&](int r) {
     try {
-      rank_main(cfg, r, sh, hub, ids, use_rccl);
+      rank_main(cfg, r, sh, hub, ids, use_rccl, hb);
     } catch (const Error& e) {
       hub->fail(e.what());
       std::lock_guard<std::mutex> lk(sh.mu);
@@ -285,6 +291,11 @@ RunReport run_local(const RunConfig& cfg) {
     std::vector<std::thread> th;
     for (int r = 0; r < cfg.ranks; ++r) th.emplace_back([&, r] { guarded(r); });
     for (auto& t : th) t.join();
+  }
+  if (hb) {
+    sh.rep.race_count = hb->races();
+    sh.rep.races = hb->reports();
+    sh.rep.race_ops = hb->ops();
   }
   return sh.rep;
 }

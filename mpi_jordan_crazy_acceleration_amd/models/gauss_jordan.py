@@ -49,6 +49,7 @@ class GaussJordan:
     sync_debug: bool = False
     residual: str = "always"
     host_threads: int = 0
+    race_check: bool = False  # happens-before schedule checker (RaceCheckDevice): report["races"]
     extra: dict = field(default_factory=dict)
 
     def _cfg(self, n: int) -> dict:
@@ -58,7 +59,8 @@ class GaussJordan:
                    pivot=self.pivot,
                    eps=float(self.eps),
                    sync_debug=bool(self.sync_debug), residual=self.residual,
-                   host_threads=int(self.host_threads), jitter_us=float(self.jitter_us))
+                   host_threads=int(self.host_threads), jitter_us=float(self.jitter_us),
+                   race_check=bool(self.race_check))
         cfg.update(self.extra)
         return cfg
 
