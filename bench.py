@@ -20,7 +20,10 @@ every collective of the solve is RCCL, issued by the native engine from C++.
 
 Failure handling: every host wait of the engine is bounded by ``--comm-timeout`` (default 90 s,
 below the driver's 600 s), so a hung peer turns into a non-zero exit on every rank, each naming
-its step, phase and the collective it sat in.
+its step, phase and the collective it sat in.  A wrong inverse is a failure too: after the timed
+loop the residual ||A A^-1 - I||_inf (the reference's check, main.cpp:490-507) is compared with
+``utils.metrics.residual_bound`` for the generator and size; non-finite or above the bound, the
+JSON line says ``"check": "residual_failed"`` and every rank exits 2.
 
 ``--same-gpu`` (rehearsal on a one-GPU box): all ranks share device 0 and RCCL is told that every
 rank is its own host (``NCCL_HOSTID``), so it accepts the duplicate device and connects the ranks
@@ -261,6 +264,13 @@ def run_rank(args) -> int:
         except RuntimeError as e:
             return fail(e)
     gflops = 2.0 * float(args.n) ** 3 / (ms / 1e3) / 1e9
+    from mpi_jordan_crazy_acceleration_amd.utils.metrics import residual_bound, residual_ok
+
+    bound = residual_bound(args.gen, args.n, args.dtype)
+    if args.no_residual:
+        check = "skipped"
+    else:
+        check = "residual_ok" if residual_ok(res, args.gen, args.n, args.dtype) else "residual_failed"
     if rank == 0:
         pol = dict(mine["policy"])
         solve_all = [x for e in everyone for x in e["solve_s"]]
@@ -304,6 +314,8 @@ def run_rank(args) -> int:
             "host_wait_ms_max": round(max(e["host_wait_ms"] for e in everyone), 3),
             "host_wait_ms": round(st["host_wait_ms"], 3),
             "residual_inf": res,
+            "residual_bound": bound,
+            "check": check,
             "status": st["status"],
             "offdiag_pivots": st["offdiag_pivots"],
             "pivot_fallbacks": st.get("pivot_fallbacks", 0),
@@ -324,6 +336,10 @@ def run_rank(args) -> int:
         print(json.dumps(out), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
+    if check == "residual_failed":
+        print(f"bench.py: rank {rank}: residual {res} exceeds the bound {bound} for --gen {args.gen} "
+              f"N={args.n} {args.dtype}: wrong inverse", file=sys.stderr, flush=True)
+        return 2
     return 0
 
 

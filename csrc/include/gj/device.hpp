@@ -152,15 +152,19 @@ class Device {
   // compute inv(W) by Gauss-Jordan with partial pivoting (reference inverse_block, main.cpp:746-820),
   // write it transposed to inv_t[b*m*m + j*m + i] = inv(W)[i][j], its inf-norm to scores[b]
   // (block_norm, main.cpp:669-683), and valid[b] (0 when singular: |pivot| < thresh).
+  // nlive = the number of local blocks with used == 0 (the caller knows every earlier pivot):
+  // devices launch one workgroup per LIVE candidate only, so no used block is dispatched (its
+  // workgroup would hold a whole CU's LDS / wave slots for nothing); scores / valid of used blocks
+  // are then left as they were (every consumer skips used blocks).  nlive < 0: all nblk.
   virtual void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
-                             int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                             int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
                              int s) = 0;
   // block_inverse with the pivot selection run by the launch's last workgroup (PivotSelectArgs:
   // p > 1 the local argmin -> *sel.rec, like pivot_local; p == 1 the whole pivot_select_single).
   // Returns false, having enqueued nothing, where the device or the kernel family it would use
   // cannot fuse them; the caller then runs block_inverse and the selection as separate launches.
   virtual bool block_inverse_select(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
-                                    int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                                    int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
                                     const PivotSelectArgs& sel, int s) {
     (void)dt; (void)Lt; (void)ldl; (void)inv_t; (void)scores; (void)valid; (void)used; (void)L;
     (void)thresh; (void)sel; (void)s;

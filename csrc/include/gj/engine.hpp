@@ -274,6 +274,7 @@ class Engine {
   double* dhost_ = nullptr;
   int64_t ihost_len_ = 0;
   PivotResult piv_[2][kMaxDepth];      // pivots of the panels in flight (by panel parity)
+  int64_t live_ = 0;                   // local block rows not yet used as a pivot row (candidates)
 
   // events
   int ev_L_ = -1, ev_main_ = -1, ev_sel_[2] = {-1, -1}, ev_edit_[2] = {-1, -1};
@@ -296,6 +297,7 @@ class Engine {
   int64_t cur_step_ = -1;
   const char* cur_phase_ = "setup";
   int64_t hang_step_ = -1;  // GJ_TEST_HANG (fault injection)
+  int64_t corrupt_step_ = -1;  // GJ_TEST_CORRUPT (a wrong inverse on purpose)
   // GJ_TEST_DROP_WAIT=<name>[,<name>]: leave out one ordering edge of the schedule (a planted
   // hazard the happens-before checker must report; tests only): "cp" the SIDE wait for the chunk
   // pass two panels back, "edit" MAIN's wait for the owner edits, "b" MAIN's wait for a chunk's

@@ -43,10 +43,10 @@ class HostDevice : public Device {
                      int64_t col0, int64_t m, int s) override;
   void add_diag(DType dt, void* A, int64_t ld, int64_t nd, double alpha, int s) override;
   void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
-                     int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                     int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
                      int s) override;
   bool block_inverse_select(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
-                            int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                            int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
                             const PivotSelectArgs& sel, int s) override;
   void candidate_maxabs(DType dt, const void* Lt, int64_t ldl, double* scores, int32_t* valid,
                         const int32_t* used, const Layout& L, double thresh, int s) override;

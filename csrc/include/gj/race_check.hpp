@@ -194,9 +194,9 @@ class RaceCheckDevice : public Device {
                      int64_t m, int s) override;
   void add_diag(DType dt, void* A, int64_t ld, int64_t nd, double alpha, int s) override;
   void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,
-                     const int32_t* used, const Layout& L, double thresh, int s) override;
+                     const int32_t* used, const Layout& L, double thresh, int64_t nlive, int s) override;
   bool block_inverse_select(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
-                            int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                            int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
                             const PivotSelectArgs& sel, int s) override;
   void set_block_inverse_hint(int variant) override { inner_->set_block_inverse_hint(variant); }
   size_t block_inverse_scratch_bytes(DType dt, const Layout& L, int variant) const override {

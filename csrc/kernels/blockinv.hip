@@ -70,17 +70,18 @@ __global__ __launch_bounds__(NTH) void block_inverse_kernel(const T* __restrict_
                                                             int32_t* __restrict__ valid,
                                                             const int32_t* __restrict__ used,
                                                             int m, int64_t p, int64_t k,
-                                                            double thresh, int32_t* __restrict__ piv_out) {
+                                                            double thresh, int32_t* __restrict__ piv_out,
+                                                            int live_nblk) {
   constexpr int TR = NTH / 32;   // thread rows (column groups)
   constexpr int RI = MP / 32;    // rows per thread
   constexpr int CJ = MP / TR;    // columns per thread
   constexpr int SCAN = (MP + 63) / 64;
   static_assert(RI >= 1 && CJ >= 1, "bad geometry");
 
-  const int b = blockIdx.x;
+  const int b = live_nblk ? live_block(used, live_nblk, p, k) : (int)blockIdx.x;  // see live_block
   const int64_t g = (int64_t)b * p + k;
-  if (used[g]) {
-    if (threadIdx.x == 0) {
+  if (b < 0 || used[g]) {
+    if (threadIdx.x == 0 && b >= 0) {
       valid[b] = 0;
       scores[b] = 0.0;
     }
@@ -287,12 +288,12 @@ __global__ __launch_bounds__(256) void block_inverse_generic(const T* __restrict
                                                              const int32_t* __restrict__ used,
                                                              int m, int64_t p, int64_t k,
                                                              double thresh, T* scratch,
-                                                             int* iscratch) {
-  const int b = blockIdx.x;
+                                                             int* iscratch, int live_nblk) {
+  const int b = live_nblk ? live_block(used, live_nblk, p, k) : (int)blockIdx.x;  // see live_block
   const int64_t g = (int64_t)b * p + k;
   const int tid = threadIdx.x;
-  if (used[g]) {
-    if (tid == 0) {
+  if (b < 0 || used[g]) {
+    if (tid == 0 && b >= 0) {
       valid[b] = 0;
       scores[b] = 0.0;
     }
@@ -443,12 +444,12 @@ __global__ __launch_bounds__(256) void block_inverse_blocked(const T* __restrict
                                                              int32_t* __restrict__ valid,
                                                              const int32_t* __restrict__ used, int m, int64_t p,
                                                              int64_t k, double thresh, T* __restrict__ scratch,
-                                                             int32_t* __restrict__ piv_out) {
+                                                             int32_t* __restrict__ piv_out, int live_nblk) {
   extern __shared__ __attribute__((aligned(16))) unsigned char bb_smem[];
-  const int b = blockIdx.x;
+  const int b = live_nblk ? live_block(used, live_nblk, p, k) : (int)blockIdx.x;  // see live_block
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (used[(int64_t)b * p + k]) {
-    if (tid == 0) {
+  if (b < 0 || used[(int64_t)b * p + k]) {
+    if (tid == 0 && b >= 0) {
       valid[b] = 0;
       scores[b] = 0.0;
     }
@@ -698,10 +699,11 @@ __global__ __launch_bounds__(256) void block_inverse_blocked(const T* __restrict
 
 template <typename T>
 static bool launch_blocked(const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,
-                           const int32_t* used, const Layout& L, double thresh, hipStream_t s, void* scratch) {
+                           const int32_t* used, const Layout& L, double thresh, int64_t nlive, hipStream_t s, void* scratch) {
   const int m = (int)L.m;
   if (m <= 256 || m > 1024) return false;
-  const unsigned grid = (unsigned)L.nblk;
+  const unsigned grid = (unsigned)(nlive >= 0 ? std::max<int64_t>(nlive, 1) : L.nblk);
+  const int live_nblk = nlive >= 0 ? (int)L.nblk : 0;
   const int RPT = (m + 255) / 256;
   const int PBv = RPT <= 2 ? 16 : 8;
   const size_t lds = (size_t)m * PBv * sizeof(T) + 4 * (size_t)m * sizeof(int);
@@ -718,7 +720,7 @@ static bool launch_blocked(const void* Lt, int64_t ldl, void* inv_t, double* sco
       attr = true;                                                                                    \
     }                                                                                                 \
     hipLaunchKernelGGL((block_inverse_blocked<T, RP, PBB>), dim3(grid), dim3(256), lds, s, lt, ldl,   \
-                       it, scores, valid, used, m, L.p, L.k, thresh, sc, probe);                      \
+                       it, scores, valid, used, m, L.p, L.k, thresh, sc, probe, live_nblk);           \
   } while (0)
   if (RPT == 2) GJ_BB(2, 16);
   else if (RPT == 3) GJ_BB(3, 8);
@@ -744,40 +746,41 @@ int block_inverse_variant() { return bi_variant(); }
 
 template <typename T>
 static void launch_bi(const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,
-                      const int32_t* used, const Layout& L, double thresh, hipStream_t s,
+                      const int32_t* used, const Layout& L, double thresh, int64_t nlive, hipStream_t s,
                       void* scratch, int* iscratch, int variant) {
   const int m = (int)L.m;
-  const unsigned grid = (unsigned)L.nblk;
+  const unsigned grid = (unsigned)(nlive >= 0 ? std::max<int64_t>(nlive, 1) : L.nblk);
+  const int live_nblk = nlive >= 0 ? (int)L.nblk : 0;
   const T* lt = static_cast<const T*>(Lt);
   T* it = static_cast<T*>(inv_t);
   const int g_bi_variant = variant >= 0 ? variant : bi_variant();
   if (g_bi_variant == 5 && block_inverse_co(sizeof(T) == 8 ? DType::F64 : DType::F32, Lt, ldl, inv_t, scores,
-                                            valid, used, L, thresh, s, scratch))
+                                            valid, used, L, thresh, nlive, s, scratch))
     return;
   if (g_bi_variant == 0 &&
       block_inverse_mfma(sizeof(T) == 8 ? DType::F64 : DType::F32, Lt, ldl, inv_t, scores, valid, used,
-                         L, thresh, s))
+                         L, thresh, nlive, s))
     return;
   if (g_bi_variant != 1 && block_inverse_big(sizeof(T) == 8 ? DType::F64 : DType::F32, Lt, ldl, inv_t, scores,
-                                              valid, used, L, thresh, s, scratch))
+                                              valid, used, L, thresh, nlive, s, scratch))
     return;
   if (m <= 32)
     hipLaunchKernelGGL((block_inverse_kernel<T, 32, 256>), dim3(grid), dim3(256), 0, s, lt, ldl, it,
-                       scores, valid, used, m, L.p, L.k, thresh, block_inverse_probe());
+                       scores, valid, used, m, L.p, L.k, thresh, block_inverse_probe(), live_nblk);
   else if (m <= 64)
     hipLaunchKernelGGL((block_inverse_kernel<T, 64, 256>), dim3(grid), dim3(256), 0, s, lt, ldl, it,
-                       scores, valid, used, m, L.p, L.k, thresh, block_inverse_probe());
+                       scores, valid, used, m, L.p, L.k, thresh, block_inverse_probe(), live_nblk);
   else if (m <= 128)  // 16 elements per thread, 4 waves per SIMD to hide the per-step latency chain
     hipLaunchKernelGGL((block_inverse_kernel<T, 128, 1024>), dim3(grid), dim3(1024), 0, s, lt, ldl,
-                       it, scores, valid, used, m, L.p, L.k, thresh, block_inverse_probe());
+                       it, scores, valid, used, m, L.p, L.k, thresh, block_inverse_probe(), live_nblk);
   else if (m <= 256 && sizeof(T) == 4)  // 256x256 fp32 = 64 VGPRs/lane at 1024 threads
     hipLaunchKernelGGL((block_inverse_kernel<T, 256, 1024>), dim3(grid), dim3(1024), 0, s, lt, ldl,
-                       it, scores, valid, used, m, L.p, L.k, thresh, block_inverse_probe());
-  else if (g_bi_variant != 6 && launch_blocked<T>(Lt, ldl, inv_t, scores, valid, used, L, thresh, s, scratch))
+                       it, scores, valid, used, m, L.p, L.k, thresh, block_inverse_probe(), live_nblk);
+  else if (g_bi_variant != 6 && launch_blocked<T>(Lt, ldl, inv_t, scores, valid, used, L, thresh, nlive, s, scratch))
     return;
   else
     hipLaunchKernelGGL((block_inverse_generic<T>), dim3(grid), dim3(256), 0, s, lt, ldl, it, scores,
-                       valid, used, m, L.p, L.k, thresh, static_cast<T*>(scratch), iscratch);
+                       valid, used, m, L.p, L.k, thresh, static_cast<T*>(scratch), iscratch, live_nblk);
 }
 
 // The kernel launch_bi picks (same decision tree), for the engine's policy report.
@@ -806,21 +809,21 @@ size_t block_inverse_iscratch_bytes(const Layout& L) {
 }
 
 bool block_inverse_select(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
-                          int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                          int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
                           hipStream_t s, const PivotSelectArgs& sel, int variant) {
   const int v = variant >= 0 ? variant : bi_variant();
   if (v != 0 || L.nblk <= 0) return false;
-  return block_inverse_mfma(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, s, &sel);
+  return block_inverse_mfma(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, nlive, s, &sel);
 }
 
 void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
-                   int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                   int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
                    hipStream_t s, void* scratch, int* iscratch, int variant) {
   if (L.nblk <= 0) return;
   if (dt == DType::F64)
-    launch_bi<double>(Lt, ldl, inv_t, scores, valid, used, L, thresh, s, scratch, iscratch, variant);
+    launch_bi<double>(Lt, ldl, inv_t, scores, valid, used, L, thresh, nlive, s, scratch, iscratch, variant);
   else
-    launch_bi<float>(Lt, ldl, inv_t, scores, valid, used, L, thresh, s, scratch, iscratch, variant);
+    launch_bi<float>(Lt, ldl, inv_t, scores, valid, used, L, thresh, nlive, s, scratch, iscratch, variant);
 }
 
 }  // namespace kern

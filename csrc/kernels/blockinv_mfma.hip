@@ -92,7 +92,7 @@ template <typename T, int MP, int LAY = 0>
 __global__ __launch_bounds__(64 * (MP / 16 + 1 + (LAY ? (MP / 16 - 1) / 3 : 0))) void block_inverse_mfma_kernel(
     const T* __restrict__ Lt, int64_t ldl, T* __restrict__ inv_t, double* __restrict__ scores,
     int32_t* __restrict__ valid, const int32_t* __restrict__ used, int m, int64_t p, int64_t k,
-    double thresh, int32_t* __restrict__ piv_out, PivotSelectArgs sel) {
+    double thresh, int32_t* __restrict__ piv_out, PivotSelectArgs sel, int live_nblk) {
   using TL = BiTile<T>;
   using acc_t = typename TL::acc_t;
   constexpr int NW = MP / 16;     // block waves = row tiles = panels
@@ -106,14 +106,16 @@ __global__ __launch_bounds__(64 * (MP / 16 + 1 + (LAY ? (MP / 16 - 1) / 3 : 0)))
   static_assert(NW * 16 == MP && PER * NW == 16, "MP must be 32, 64 or 128");
   static_assert(SR * LDS_S <= 4 * MP * LDR, "staging does not fit");
 
-  const int b = blockIdx.x;
-  if (used[(int64_t)b * p + k]) {
+  // live_nblk > 0: the grid covers only the live candidates (live_block); 0: one per local block
+  const int nblk = live_nblk ? live_nblk : (int)gridDim.x;
+  const int b = live_nblk ? live_block(used, live_nblk, p, k) : (int)blockIdx.x;
+  if (b < 0 || used[(int64_t)b * p + k]) {
     if (threadIdx.x < 64) {
-      if (threadIdx.x == 0) {
+      if (threadIdx.x == 0 && b >= 0) {
         valid[b] = 0;
         scores[b] = 0.0;
       }
-      select_tail(sel, scores, valid, used, gridDim.x, p, k);
+      select_tail(sel, scores, valid, used, nblk, p, k);
     }
     return;
   }
@@ -401,7 +403,7 @@ __global__ __launch_bounds__(64 * (MP / 16 + 1 + (LAY ? (MP / 16 - 1) / 3 : 0)))
         valid[b] = 0;
         scores[b] = 0.0;
       }
-      select_tail(sel, scores, valid, used, gridDim.x, p, k);
+      select_tail(sel, scores, valid, used, nblk, p, k);
     }
     return;
   }
@@ -418,7 +420,7 @@ __global__ __launch_bounds__(64 * (MP / 16 + 1 + (LAY ? (MP / 16 - 1) / 3 : 0)))
       scores[b] = mx;
       valid[b] = isfinite(mx) ? 1 : 0;
     }
-    select_tail(sel, scores, valid, used, gridDim.x, p, k);
+    select_tail(sel, scores, valid, used, nblk, p, k);
   }
 }
 
@@ -427,12 +429,14 @@ void set_block_inverse_probe(int32_t* piv_out) { g_piv_probe = piv_out; }
 int32_t* block_inverse_probe() { return g_piv_probe; }
 
 bool block_inverse_mfma(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
-                        int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                        int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
                         hipStream_t s, const PivotSelectArgs* sel) {
   const int m = (int)L.m;
   if (m <= 16 || m > 128) return false;
-  const unsigned grid = (unsigned)L.nblk;
-  if (grid == 0) return true;
+  if (L.nblk == 0) return true;
+  // one workgroup per live candidate (at least one: the fused selection tail must run)
+  const unsigned grid = (unsigned)(nlive >= 0 ? std::max<int64_t>(nlive, 1) : L.nblk);
+  const int live_nblk = nlive >= 0 ? (int)L.nblk : 0;
   const int MP = m <= 32 ? 32 : m <= 64 ? 64 : 128;
   const PivotSelectArgs tail = sel ? *sel : PivotSelectArgs{};
   // MP = 128: the pivot wave alone on its SIMD (LAY 1), where 8 block waves' MFMAs would share it:
@@ -440,7 +444,7 @@ bool block_inverse_mfma(DType dt, const void* Lt, int64_t ldl, void* inv_t, doub
 #define GJ_BI_LAUNCH(T, MPV, LAYV)                                                                       \
   hipLaunchKernelGGL((block_inverse_mfma_kernel<T, MPV, LAYV>), dim3(grid), dim3(64 * bim_hw_waves<MPV, LAYV>()), \
                      0, s, static_cast<const T*>(Lt), ldl, static_cast<T*>(inv_t), scores, valid, used, m, L.p,   \
-                     L.k, thresh, g_piv_probe, tail)
+                     L.k, thresh, g_piv_probe, tail, live_nblk)
   if (dt == DType::F64) {
     if (MP == 32) GJ_BI_LAUNCH(double, 32, 0);
     else if (MP == 64) GJ_BI_LAUNCH(double, 64, 0);

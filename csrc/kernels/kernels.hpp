@@ -37,17 +37,17 @@ void commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* va
 
 // blockinv.hip
 void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
-                   int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                   int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
                    hipStream_t s, void* scratch, int* iscratch, int variant = -1);
 // blockinv_mfma.hip: 16 < m <= 128 (false = not handled)
 bool block_inverse_mfma(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
-                        int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                        int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
                         hipStream_t s, const PivotSelectArgs* sel = nullptr);
 // block_inverse with the pivot selection fused into the launch (PivotSelectArgs) where the kernel
 // family the call resolves to supports it (the matrix-core register kernel); false = nothing was
 // launched, the caller runs block_inverse and the selection separately
 bool block_inverse_select(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
-                          int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                          int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
                           hipStream_t s, const PivotSelectArgs& sel, int variant = -1);
 // test probe: when set, the matrix-core block inverses write the pivot row of every column of
 // every candidate to piv_out[b * m + c] (device memory; nullptr = off)
@@ -55,11 +55,11 @@ void set_block_inverse_probe(int32_t* piv_out);
 int32_t* block_inverse_probe();
 // blockinv_big.hip: fp64 128 < m <= 256 (false = not handled); scratch: nblk 256 x 256 images
 bool block_inverse_big(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,
-                       const int32_t* used, const Layout& L, double thresh, hipStream_t s, void* scratch);
+                       const int32_t* used, const Layout& L, double thresh, int64_t nlive, hipStream_t s, void* scratch);
 size_t block_inverse_big_scratch_bytes(DType dt, const Layout& L);
 // the co-resident form (4 waves, fits the slot one trailing-update workgroup frees): fp64 32 < m <= 128
 bool block_inverse_co(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,
-                      const int32_t* used, const Layout& L, double thresh, hipStream_t s, void* scratch);
+                      const int32_t* used, const Layout& L, double thresh, int64_t nlive, hipStream_t s, void* scratch);
 // scratch needed by the fp64 m > 128 paths (big kernel / generic sweep)
 // (variant: the kernel family to use for this call, -1 = the process-wide setting)
 size_t block_inverse_scratch_bytes(DType dt, const Layout& L, int variant = -1);

@@ -144,5 +144,38 @@ __device__ __forceinline__ T fast_recip(T x) {
   }
 }
 
+// The candidate of this workgroup when the launch covers only the LIVE candidates (grid = this
+// rank's count of local block rows that have not served as a pivot row, Device::block_inverse
+// nlive): the blockIdx.x-th local block b < nblk with used[b p + k] == 0, or -1 past the last.
+// Every wave computes it (uniform, no barrier); the used flags are read 256 at a time so the
+// loads of a pass are in flight together (one pass for the 256 blocks of N = 32768 at p = 1).
+// Reference: only rows >= t are candidates (main.cpp:1028-1039); a dispatched dead workgroup
+// would hold a whole CU's LDS and wave slots until it exits.
+__device__ __forceinline__ int live_block(const int32_t* __restrict__ used, int nblk, int64_t p, int64_t k) {
+  const int want = (int)blockIdx.x;
+  const int lane = (int)(threadIdx.x & 63);
+  int base = 0;
+  for (int b0 = 0; b0 < nblk; b0 += 256) {
+    bool lv[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int b = b0 + 64 * s + lane;
+      lv[s] = b < nblk && used[(int64_t)b * p + k] == 0;
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const uint64_t bal = __ballot(lv[s]);
+      const int cnt = __popcll(bal);
+      if (want < base + cnt) {
+        const int below = __popcll(bal & ((1ull << lane) - 1ull));
+        const uint64_t hit = __ballot(lv[s] && below == want - base);
+        return b0 + 64 * s + __ffsll((unsigned long long)hit) - 1;
+      }
+      base += cnt;
+    }
+  }
+  return -1;
+}
+
 }  // namespace kern
 }  // namespace gj

@@ -248,11 +248,14 @@ PYBIND11_MODULE(_C, mod) {
            })
       .def("block_inverse",
            [lay](Device& d, const std::string& dt, U Lt, int64_t ldl, U inv_t, U scores, U valid,
-                 U used, int64_t n, int64_t m, int64_t p, int64_t k, double thresh) {
+                 U used, int64_t n, int64_t m, int64_t p, int64_t k, double thresh, int64_t nlive) {
              d.block_inverse(parse_dtype(dt), (const void*)Lt, ldl, (void*)inv_t, (double*)scores,
-                             (int32_t*)valid, (const int32_t*)used, lay(n, m, p, k), thresh, S_MAIN);
+                             (int32_t*)valid, (const int32_t*)used, lay(n, m, p, k), thresh, nlive, S_MAIN);
              d.sync_stream(S_MAIN);
-           })
+           },
+           py::arg("dt"), py::arg("Lt"), py::arg("ldl"), py::arg("inv_t"), py::arg("scores"), py::arg("valid"),
+           py::arg("used"), py::arg("n"), py::arg("m"), py::arg("p"), py::arg("k"), py::arg("thresh"),
+           py::arg("nlive") = -1)
       // pivot selection kernels (tests): local argmin of one rank's candidates -> 32-B record at rec
       .def("pivot_local",
            [lay](Device& d, U scores, U valid, U used, U pos, int64_t n, int64_t m, int64_t p, int64_t k, U rec) {
@@ -273,21 +276,24 @@ PYBIND11_MODULE(_C, mod) {
       // stream between two timing events (no host work in between); returns microseconds per call.
       .def("time_block_inverse",
            [lay](Device& d, const std::string& dt, U Lt, int64_t ldl, U inv_t, U scores, U valid,
-                 U used, int64_t n, int64_t m, int64_t p, int64_t k, double thresh, int reps) {
+                 U used, int64_t n, int64_t m, int64_t p, int64_t k, double thresh, int reps, int64_t nlive) {
              py::gil_scoped_release rel;
              const Layout L = lay(n, m, p, k);
              const DType t = parse_dtype(dt);
              d.block_inverse(t, (const void*)Lt, ldl, (void*)inv_t, (double*)scores, (int32_t*)valid,
-                             (const int32_t*)used, L, thresh, S_SIDE);
+                             (const int32_t*)used, L, thresh, nlive, S_SIDE);
              const int e0 = d.create_event(true), e1 = d.create_event(true);
              d.record(e0, S_SIDE);
              for (int i = 0; i < reps; ++i)
                d.block_inverse(t, (const void*)Lt, ldl, (void*)inv_t, (double*)scores, (int32_t*)valid,
-                               (const int32_t*)used, L, thresh, S_SIDE);
+                               (const int32_t*)used, L, thresh, nlive, S_SIDE);
              d.record(e1, S_SIDE);
              d.sync_stream(S_SIDE);
              return 1e3 * d.event_ms(e0, e1) / std::max(reps, 1);
-           })
+           },
+           py::arg("dt"), py::arg("Lt"), py::arg("ldl"), py::arg("inv_t"), py::arg("scores"), py::arg("valid"),
+           py::arg("used"), py::arg("n"), py::arg("m"), py::arg("p"), py::arg("k"), py::arg("thresh"),
+           py::arg("reps"), py::arg("nlive") = -1)
       .def("permute_blocks",
            [](Device& d, const std::string& dt, U dst, int64_t ldd, U X, int64_t ldx, int64_t nblk,
               int64_t m, int64_t Nr, U dst_blk, U colsrc) {

@@ -237,15 +237,15 @@ void AsyncHostDevice::add_diag(DType dt, void* A, int64_t ld, int64_t nd, double
 }
 void AsyncHostDevice::block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                                     int32_t* valid, const int32_t* used, const Layout& L,
-                                    double thresh, int s) {
-  enqueue(s, [=] { inner_.block_inverse(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, s); });
+                                    double thresh, int64_t nlive, int s) {
+  enqueue(s, [=] { inner_.block_inverse(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, nlive, s); });
 }
 bool AsyncHostDevice::block_inverse_select(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
-                                           int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                                           int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
                                            const PivotSelectArgs& sel, int s) {
   if (L.m <= 16 || L.m > 128 || L.nblk <= 0) return false;  // = HostDevice's range
   enqueue(s, [=] {
-    inner_.block_inverse(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, s);
+    inner_.block_inverse(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, nlive, s);
     inner_.pivot_local(scores, valid, used, sel.pos, L, sel.rec, s);
     if (sel.single) pivot_global_now(sel.rec, 1, sel.t, sel.pos_w, sel.phys_at, sel.used_w, sel.seq, sel.out,
                                      sel.host_out, s);

@@ -236,7 +236,7 @@ void HipDevice::prepare_block_inverse(DType dt, const Layout& L, int variant) {
   scratch(kern::block_inverse_iscratch_bytes(L), 1);
 }
 void HipDevice::block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
-                              int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                              int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
                               int s) {
   void* sc = nullptr;
   int* isc = nullptr;
@@ -246,13 +246,13 @@ void HipDevice::block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t
     sc = scratch(b1, 0);
     isc = static_cast<int*>(scratch(kern::block_inverse_iscratch_bytes(L), 1));
   }
-  kern::block_inverse(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, hs(streams_[s]), sc, isc, variant);
+  kern::block_inverse(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, nlive, hs(streams_[s]), sc, isc, variant);
   check_launch();
 }
 bool HipDevice::block_inverse_select(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
-                                     int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                                     int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
                                      const PivotSelectArgs& sel, int s) {
-  if (!kern::block_inverse_select(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, hs(streams_[s]), sel,
+  if (!kern::block_inverse_select(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, nlive, hs(streams_[s]), sel,
                                   bi_hint_))
     return false;
   check_launch();

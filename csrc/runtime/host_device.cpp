@@ -202,7 +202,7 @@ void HostDevice::add_diag(DType dt, void* A, int64_t ld, int64_t nd, double alph
 }
 
 void HostDevice::block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
-                               int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                               int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
                                int) {
   const int64_t m = L.m;
   parallel_for(L.nblk, nthreads_, [&](int64_t b) {
@@ -248,10 +248,10 @@ void HostDevice::block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_
 // The fused candidate-inverse + selection launch of the GPU (Device::block_inverse_select), for the
 // same kernel family range (16 < m <= 128), so the CPU executes the GPU's op sequence.
 bool HostDevice::block_inverse_select(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
-                                      int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                                      int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
                                       const PivotSelectArgs& sel, int s) {
   if (L.m <= 16 || L.m > 128 || L.nblk <= 0) return false;
-  block_inverse(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, s);
+  block_inverse(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, nlive, s);
   pivot_local(scores, valid, used, sel.pos, L, sel.rec, s);
   if (sel.single)
     pivot_global(sel.rec, 1, sel.t, sel.pos_w, sel.phys_at, sel.used_w, sel.seq, sel.out, sel.host_out, s);

@@ -511,16 +511,16 @@ void inverse_acc(std::vector<Acc>& a, DType dt, const void* Lt, int64_t ldl, voi
 }  // namespace
 
 void RaceCheckDevice::block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
-                                    int32_t* valid, const int32_t* used, const Layout& L, double thresh, int s) {
+                                    int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive, int s) {
   std::vector<Acc> a;
   inverse_acc(a, dt, Lt, ldl, inv_t, scores, valid, used, L);
   check(s, "block_inverse", a);
-  inner_->block_inverse(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, s);
+  inner_->block_inverse(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, nlive, s);
 }
 bool RaceCheckDevice::block_inverse_select(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
-                                           int32_t* valid, const int32_t* used, const Layout& L, double thresh,
+                                           int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
                                            const PivotSelectArgs& sel, int s) {
-  if (!inner_->block_inverse_select(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, sel, s)) return false;
+  if (!inner_->block_inverse_select(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, nlive, sel, s)) return false;
   std::vector<Acc> a;
   inverse_acc(a, dt, Lt, ldl, inv_t, scores, valid, used, L);
   const int64_t nr = (int64_t)sizeof(int32_t) * L.Nr;

@@ -48,7 +48,10 @@ namespace {
 //   GJ_TEST_ALLOC_FAIL  tag = matrix | block | residual | residual_stream | residual64: that rank's
 //                       allocation of that stage fails;
 //   GJ_TEST_HANG        tag = a step number: that rank never issues the pivot exchange of that
-//                       step (a rank stuck in, or dead before, a collective).
+//                       step (a rank stuck in, or dead before, a collective);
+//   GJ_TEST_CORRUPT     tag = a step number: that rank zeroes its copy of the step's normalised
+//                       pivot row in the first chunk it updates (a wrong inverse that must fail
+//                       the residual check, bench.py / --check-residual).
 bool injected(const char* var, int rank, const std::string& tag) {
   const char* e = std::getenv(var);
   if (!e || !*e) return false;
@@ -64,8 +67,9 @@ bool injected(const char* var, int rank, const std::string& tag) {
   return false;
 }
 bool injected_alloc_fail(int rank, const char* stage) { return injected("GJ_TEST_ALLOC_FAIL", rank, stage); }
-int64_t injected_hang_step(int rank) {
-  const char* e = std::getenv("GJ_TEST_HANG");
+// `var`=<rank>:<step>[,...]: the step named for this rank (-1: none).
+int64_t injected_step(const char* var, int rank) {
+  const char* e = std::getenv(var);
   if (!e || !*e) return -1;
   const std::string all = e;
   for (size_t b = 0; b <= all.size();) {
@@ -146,7 +150,8 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   }
 
   comm_.set_timeout(opt_.comm_timeout_s);
-  hang_step_ = injected_hang_step(L_.k);
+  hang_step_ = injected_step("GJ_TEST_HANG", L_.k);
+  corrupt_step_ = injected_step("GJ_TEST_CORRUPT", L_.k);
   if (const char* e = std::getenv("GJ_TEST_DROP_WAIT")) drop_wait_ = std::string(",") + e + ",";
   dev_.trace_context(&cur_step_, &cur_phase_);  // names the step / phase in schedule-check reports
   // Allocation, agreed on every rank BEFORE any other collective (reference main.cpp:366-381 and
@@ -555,7 +560,7 @@ void Engine::select(int64_t t, const void* Lt, bool full) {
     dev_.pivot_local(scores_, valid_, used_, pos_, L_, myrec_, S_SIDE);
     dev_.gather_candidate(opt_.dtype, sel_, Lt, L_.rows, myrec_, L_, S_SIDE);
     dev_.set_block_inverse_hint(bi_hint_);
-    dev_.block_inverse(opt_.dtype, sel_, L_.m, inv1_, score1_, valid1_, used1_, L1_, thresh, S_SIDE);
+    dev_.block_inverse(opt_.dtype, sel_, L_.m, inv1_, score1_, valid1_, used1_, L1_, thresh, 1, S_SIDE);
     dev_.set_block_inverse_hint(-1);
     dev_.commit_candidate(opt_.dtype, inv_, inv1_, valid1_, myrec_, L_, S_SIDE);
     prof_end(PH_PIVOT, pe, S_SIDE);
@@ -585,9 +590,9 @@ void Engine::select(int64_t t, const void* Lt, bool full) {
         sa.out = piv_dev_;
         sa.host_out = &piv_host_[par];
       }
-      fused = dev_.block_inverse_select(opt_.dtype, Lt, L_.rows, inv_, scores_, valid_, used_, L_, thresh, sa,
+      fused = dev_.block_inverse_select(opt_.dtype, Lt, L_.rows, inv_, scores_, valid_, used_, L_, thresh, live_, sa,
                                         S_SIDE);
-      if (!fused) dev_.block_inverse(opt_.dtype, Lt, L_.rows, inv_, scores_, valid_, used_, L_, thresh, S_SIDE);
+      if (!fused) dev_.block_inverse(opt_.dtype, Lt, L_.rows, inv_, scores_, valid_, used_, L_, thresh, live_, S_SIDE);
       dev_.set_block_inverse_hint(-1);
     }
     if (L_.p == 1) {
@@ -688,6 +693,7 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
     }
     piv_[par][j] = r;
     st.pivots[t] = r.phys;
+    if (r.owner == L_.k) --live_;  // this rank's block row s_t is no longer a candidate
     cur_phase_ = "panel piece";
     const bool owner = (r.owner == L_.k);
     const int64_t sl = r.phys / L_.p;
@@ -901,6 +907,8 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
       bops.push_back(BcastOp{seg, (size_t)m * W * es, (int)r.owner});
     }
     flush();
+    if (i == 0 && corrupt_step_ >= t0 && corrupt_step_ < t0 + q)  // GJ_TEST_CORRUPT (tests only)
+      dev_.memset2d(chunk + (corrupt_step_ - t0) * m * W * (int64_t)es, W * es, W * es, m, S_COMM);
     dev_.record(ev_b_[par][c], S_COMM);
   }
   dev_.record(ev_cp_[par], S_COMM);
@@ -1041,6 +1049,7 @@ SolveStats Engine::solve_steps() {
   dev_.sync_stream(S_SIDE);
 
   st.pivots.assign(Nr, -1);
+  live_ = L_.nblk;
   double host_wait = 0;
   bool ok = true;
 

@@ -87,10 +87,11 @@ def extract_neg_t(X: torch.Tensor, col0: int, m: int) -> torch.Tensor:
 
 
 def block_inverse(Lt: torch.Tensor, n: int, m: int, p: int = 1, k: int = 0, used: torch.Tensor = None,
-                  thresh: float = 0.0):
+                  thresh: float = 0.0, nlive: int = -1):
     """Batched candidate inversion over the K-major multiplier panel Lt (m x rows).
 
-    Returns (inv_t [nblk, m, m] with inv_t[b] = inv(W_b)^T, scores [nblk], valid [nblk])."""
+    nlive >= 0: launch one workgroup per unused candidate only (the engine's form; scores / valid
+    of used blocks are then left untouched), -1: one per local block.  Returns (inv_t [nblk, m, m] with inv_t[b] = inv(W_b)^T, scores [nblk], valid [nblk])."""
     nblk = Lt.shape[1] // m
     dev = Lt.device
     inv_t = torch.zeros((max(nblk, 1), m, m), dtype=Lt.dtype, device=dev)
@@ -100,7 +101,7 @@ def block_inverse(Lt: torch.Tensor, n: int, m: int, p: int = 1, k: int = 0, used
     if used is None:
         used = torch.zeros(Nr, dtype=torch.int32, device=dev)
     device_for(Lt).block_inverse(_DT[Lt.dtype], _p(Lt), Lt.stride(0), _p(inv_t), _p(scores), _p(valid), _p(used),
-                                 n, m, p, k, thresh)
+                                 n, m, p, k, thresh, nlive)
     return inv_t[:nblk], scores[:nblk], valid[:nblk]
 
 

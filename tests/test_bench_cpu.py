@@ -145,3 +145,29 @@ def test_bench_hang_fails_fast(launcher):
             assert f"rank {rank}/4, step 3 of 25, phase pivot search" in e, e[-2000:]
         assert "timed out after 6" in out[2][2]
     assert time.monotonic() - t0 < 90
+
+
+def test_bench_wrong_inverse_fails():
+    """A wrong inverse is a failure, not a fast success (reference: main.cpp:490-507 prints the
+    residual, never fails on it).  GJ_TEST_CORRUPT=1:5 zeroes rank 1's copy of step 5's pivot row
+    in one chunk: the run completes, the JSON line says residual_failed, every rank exits 2."""
+    args = ("--steps", "1", "--warmup", "0", "--size", "200", "--block", "8")
+    clean = _self_launch(4, *args)
+    assert clean.returncode == 0, clean.stderr[-3000:]
+    d = _json_line(clean.stdout)
+    assert d["check"] == "residual_ok" and d["residual_inf"] < d["residual_bound"]
+    bad = _self_launch(4, *args, env_extra={"GJ_TEST_CORRUPT": "1:5"})
+    assert bad.returncode == 2, bad.stderr[-3000:]
+    d = _json_line(bad.stdout)
+    assert d["check"] == "residual_failed" and not d["residual_inf"] < d["residual_bound"]
+    assert "rank exit codes [2, 2, 2, 2]" in bad.stderr
+    assert "wrong inverse" in bad.stderr
+
+
+def test_cli_check_residual(gj_bin):
+    base = [gj_bin, "--device", "cpu", "-p", "3", "--gen", "random", "--check-residual", "1e-6", "200", "8"]
+    assert subprocess.run(base, capture_output=True, text=True, timeout=120).returncode == 0
+    r = subprocess.run(base, capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, GJ_TEST_CORRUPT="0:2"))
+    assert r.returncode == 2 and "residual check failed" in r.stderr, r.stderr
+    assert "residual:" in r.stdout  # the reference's output is still printed in full

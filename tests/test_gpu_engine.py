@@ -207,3 +207,29 @@ def test_engine_large_blocks(n, m, p, dtype):
                          comm="loopback" if p > 1 else "auto").inverse(A)
     tol = 1e-8 if dtype == "fp64" else 1e-4
     assert np.abs(inv - ref).max() / np.abs(ref).max() < tol
+
+
+@pytest.mark.parametrize("n", [8192, 8448])
+def test_depth2_p8_async_jittered(n):
+    """The configuration of the one unexplained wrong inverse (profiles/depth_pgt1.md: p = 8, m = 60,
+    depth 2, async virtual ranks on one GPU) with an explicit depth 2, jittered arrivals, at and
+    above N = 8192.  The happens-before checker finds this schedule race-free on the CPU
+    (tests/test_race_check.py); here the GPU executes it.  The residual must match one GPU's."""
+    one = gj.GaussJordan(block_size=60, ranks=1, device="gpu", depth=2).run(n, gen="random", seed=11)
+    rep = gj.GaussJordan(block_size=60, ranks=8, device="gpu", comm="async", jitter_us=50.0, depth=2).run(
+        n, gen="random", seed=11)
+    assert one["status"] == 0 and rep["status"] == 0, (one["message"], rep["message"])
+    assert rep["residual"] < 10 * one["residual"] + 1e-9, (rep["residual"], one["residual"])
+
+
+@pytest.mark.parametrize("p", [1, 4])
+def test_race_check_on_gpu(p):
+    """The schedule checker around the HIP device: the GPU's op sequence (fused candidate inverse +
+    selection, CU reservation, co-resident candidate inverse at p > 1, tuned broadcast) is race-free
+    and the wrapped run still computes the right inverse."""
+    rep = gj.GaussJordan(block_size=64, ranks=p, device="gpu", comm="async" if p > 1 else "auto",
+                         race_check=True, jitter_us=20.0).run(1500, gen="random", seed=2)
+    assert rep["status"] == 0, rep["message"]
+    assert rep["race_ops"] > 0
+    assert rep["race_count"] == 0, "\n".join(rep["races"])
+    assert rep["residual"] < 1e-8

@@ -398,3 +398,37 @@ def test_pivot_select_single_bookkeeping(native):
         h_seq[t] = s
     assert pos.cpu().tolist() == h_pos and phys_at.cpu().tolist() == h_phys
     assert used.cpu().tolist() == h_used and seq.cpu().tolist()[:40] == h_seq[:40]
+
+
+@pytest.mark.parametrize("variant,m,dtype", [("panel", 60, torch.float64), ("panel", 128, torch.float64),
+                                             ("panel", 100, torch.float32), ("co", 128, torch.float64),
+                                             ("panel", 256, torch.float64), ("panel", 300, torch.float64),
+                                             ("sweep", 64, torch.float64), ("generic", 300, torch.float64)])
+@pytest.mark.parametrize("p,k", [(1, 0), (3, 2)])
+def test_block_inverse_live_grid_matches_full_grid(native, variant, m, dtype, p, k):
+    """nlive >= 0 (the engine's launch): one workgroup per UNUSED candidate, the workgroup's block
+    found from the used flags (live_block).  Every live block's inverse, score and validity must be
+    bit-identical to the one-workgroup-per-block launch; used blocks are not touched."""
+    rng = np.random.default_rng(m + p)
+    nblk = 37
+    Nr = nblk * p
+    Lt = torch.from_numpy(rng.uniform(-1, 1, (m, nblk * m))).to(dtype).cuda()
+    used = torch.from_numpy((rng.random(Nr) < 0.5).astype(np.int32)).cuda()
+    mine = used.cpu().numpy()[k::p][:nblk]
+    live = np.flatnonzero(mine == 0)
+    native.set_block_inverse_variant(variant)
+    try:
+        full = ops.block_inverse(Lt, Nr * m, m, p, k, used=used, thresh=1e-12)
+        sentinel = [t.clone().fill_(7) for t in full]
+        inv_t, scores, valid = [t.clone() for t in sentinel]
+        device = ops.device_for(Lt)
+        device.block_inverse(ops._DT[dtype], Lt.data_ptr(), Lt.stride(0), inv_t.data_ptr(), scores.data_ptr(),
+                             valid.data_ptr(), used.data_ptr(), Nr * m, m, p, k, 1e-12, len(live))
+        torch.cuda.synchronize()
+    finally:
+        native.set_block_inverse_variant("panel")
+    assert torch.equal(valid[live], full[2][live])
+    assert torch.equal(scores[live], full[1][live])
+    assert torch.equal(inv_t[live], full[0][live])
+    dead = np.flatnonzero(mine != 0)
+    assert torch.equal(valid[dead], sentinel[2][dead]) and torch.equal(inv_t[dead], sentinel[0][dead])

@@ -57,10 +57,11 @@ def test_region_geometry_matches_brute_force():
     assert C._region_covers((0, n8, 80 * 8, 200), right)
 
 
-def _run(n, m, p, comm="async", **kw):
+def _run(n, m, p, comm="async", ok=True, **kw):
     rep = gj.GaussJordan(block_size=m, ranks=p, device="cpu", comm=comm, race_check=True, host_threads=1,
                          **kw).run(n, gen="random", seed=3)
-    assert rep["status"] == 0, rep["message"]
+    if ok:
+        assert rep["status"] == 0, rep["message"]
     return rep
 
 
@@ -105,7 +106,9 @@ def test_partial_pivot_and_sync_transport_race_free(p):
 ])
 def test_planted_hazard_is_reported(drop, buffer, monkeypatch):
     monkeypatch.setenv("GJ_TEST_DROP_WAIT", drop)
-    rep = _run(300, 20, 3, depth=2, chunk_cols=100)
+    # the asynchronous executor really runs the broken schedule: the inverse may come out wrong (or
+    # "singular"); the report must be there either way
+    rep = _run(300, 20, 3, ok=False, depth=2, chunk_cols=100)
     assert rep["race_count"] > 0
     text = "\n".join(rep["races"])
     assert buffer in text, text
