@@ -196,6 +196,10 @@ def run_rank(args) -> int:
     try:
         if not gpu:
             dev = C.host_device(args.host_threads)
+            if world > 1 and os.environ.get("GJ_TEST_HW_QUEUES"):  # the GPU path's agreement, rehearsed
+                from mpi_jordan_crazy_acceleration_amd.parallel.dist import agree_hw_queues
+
+                agree_hw_queues()
             if world > 1:
                 from mpi_jordan_crazy_acceleration_amd.parallel.dist import TorchDistComm
 
@@ -203,6 +207,10 @@ def run_rank(args) -> int:
             else:
                 comm = C.self_comm()
         elif world > 1 or args.force_rccl:
+            if world > 1:  # every rank fails together, before any RCCL communicator exists
+                from mpi_jordan_crazy_acceleration_amd.parallel.dist import agree_hw_queues
+
+                agree_hw_queues()
             ids = [[C.rccl_unique_id(), C.rccl_unique_id()] if rank == 0 else None]
             if world > 1:
                 dist.broadcast_object_list(ids, src=0)

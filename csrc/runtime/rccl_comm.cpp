@@ -41,12 +41,16 @@ RcclComm::RcclComm(const std::vector<std::string>& ids, int nranks, int rank, in
     : n_(nranks), r_(rank), device_(device) {
   GJ_REQUIRE(ids.size() == 2, "RcclComm needs two unique ids");
   {
+    // The SIDE and COMM communicators must not share an in-order hardware queue (README "Progress
+    // of the two communicators").  Every rank reads the same environment (the CLI sets it before
+    // the first HIP call; the Python launchers agree on the value first, parallel/dist.py
+    // agree_hw_queues), so this refusal happens on every rank, before any communicator exists.
     const char* q = std::getenv("GPU_MAX_HW_QUEUES");
     if (nranks > 1 && (!q || std::atoi(q) < kMinHwQueues))
-      std::fprintf(stderr,
-                   "gj: warning: GPU_MAX_HW_QUEUES=%s < %d; the SIDE and COMM communicators may share a "
-                   "hardware queue (set it before the first HIP call, see runtime_env.py)\n",
-                   q ? q : "unset", kMinHwQueues);
+      throw Error(Status::CommError, std::string("GPU_MAX_HW_QUEUES=") + (q ? q : "unset") + " < " +
+                                         std::to_string(kMinHwQueues) +
+                                         ": the SIDE and COMM communicators could share a hardware queue "
+                                         "(set it before the first HIP call, see runtime_env.py)");
   }
   (void)hipSetDevice(device_);
   for (int c = 0; c < 2; ++c) {

@@ -83,6 +83,31 @@ class TorchDistComm:
         return float(t.item())
 
 
+def agree_hw_queues(group=None, need: Optional[int] = None) -> int:
+    """Collective: the smallest hardware-queue count of any rank (runtime_env.effective_hw_queues).
+
+    The two RCCL communicators of a rank (SIDE, COMM) must not share an in-order hardware queue, or
+    a SIDE kernel spinning on a peer can block the COMM kernel that peer waits for (README
+    "Progress of the two communicators").  When some rank has fewer than ``need`` (16) queues,
+    EVERY rank raises the same explained RuntimeError here, before any RCCL communicator exists
+    (reference: collective error agreement, main.cpp:371-381) -- never a hang."""
+    from ..runtime_env import MIN_HW_QUEUES, effective_hw_queues
+
+    need = MIN_HW_QUEUES if need is None else need
+    rank = dist.get_rank(group)
+    counts = [None] * dist.get_world_size(group)
+    dist.all_gather_object(counts, effective_hw_queues(rank), group=group)
+    low = min(counts)
+    if low < need:
+        bad = [r for r, c in enumerate(counts) if c < need]
+        raise RuntimeError(
+            f"GPU_MAX_HW_QUEUES: rank(s) {bad} run with {low} hardware queues per process, the engine's "
+            f"two RCCL communicators need {need} (HIP was initialised before the package could raise it: "
+            f"set GPU_MAX_HW_QUEUES={need} in the environment, or import mpi_jordan_crazy_acceleration_amd "
+            f"before the first CUDA call)")
+    return low
+
+
 def _raise_file_status(st: int, path, what: str = "") -> None:
     if st == 3:
         raise FileNotFoundError(f"cannot open{what} {path}")
@@ -120,6 +145,7 @@ class DistributedGaussJordan:
             self.local_rank = local_rank
             self.device = C.hip_device(local_rank)
             if self.world > 1:
+                agree_hw_queues()  # every rank fails together before any RCCL communicator exists
                 obj = [[C.rccl_unique_id(), C.rccl_unique_id()] if self.rank == 0 else None]
                 dist.broadcast_object_list(obj, src=0)
                 self.comm = C.rccl_comm(obj[0], self.world, self.rank, local_rank)

@@ -171,3 +171,33 @@ def test_cli_check_residual(gj_bin):
                        env=dict(os.environ, GJ_TEST_CORRUPT="0:2"))
     assert r.returncode == 2 and "residual check failed" in r.stderr, r.stderr
     assert "residual:" in r.stdout  # the reference's output is still printed in full
+
+
+def test_bench_hw_queue_shortfall_agreed():
+    """One rank runs with too few hardware queues (HIP initialised before the package could raise
+    GPU_MAX_HW_QUEUES; faked by GJ_TEST_HW_QUEUES=1:4): every rank exits 2 with the same explained
+    message before any communicator exists -- never a hang (runtime_env.py, agree_hw_queues)."""
+    out = _ranks(3, "--steps", "1", "--warmup", "0", "--size", "90", "--block", "8",
+                 env_extra={"GJ_TEST_HW_QUEUES": "1:4"}, timeout=120)
+    for rank, (rc, o, e) in enumerate(out):
+        assert rc == 2, (rank, rc, e[-2000:])
+        assert "rank(s) [1] run with 4 hardware queues" in e, e[-2000:]
+
+
+def test_effective_hw_queues_after_early_hip_init():
+    """The recorded queue count is the one HIP started with: a program that initialised HIP (here:
+    faked by a torch whose cuda reports initialised) before the package keeps its old count."""
+    code = (
+        "import os, sys, types\n"
+        "os.environ.pop('GPU_MAX_HW_QUEUES', None)\n"
+        "fake = types.ModuleType('torch'); fake.cuda = types.SimpleNamespace(is_initialized=lambda: True)\n"
+        "sys.modules['torch'] = fake\n"
+        "sys.path.insert(0, %r)\n"
+        "import importlib.util as u\n"
+        "spec = u.spec_from_file_location('rt', %r); rt = u.module_from_spec(spec); spec.loader.exec_module(rt)\n"
+        "rt.configure_runtime_env()\n"
+        "print(rt.effective_hw_queues(), os.environ['GPU_MAX_HW_QUEUES'])\n"
+    ) % (ROOT, os.path.join(ROOT, "mpi_jordan_crazy_acceleration_amd", "runtime_env.py"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split() == ["4", "16"]

@@ -89,3 +89,23 @@ def test_torchrun_cli_two_ranks_same_gpu():
     assert two[:-1] == one[:-1]  # A and inverse corners (2 decimals), "inverse matrix:"
     r1, r2 = float(one[-1].split()[1]), float(two[-1].split()[1])
     assert two[-1].startswith("residual: ") and r2 < 1e-6 and r2 <= 10 * r1 + 1e-12
+
+
+def test_hw_queue_shortfall_after_early_hip_init():
+    """Deadlock-freedom of the two communicators needs 16 hardware queues per process (README
+    "Progress of the two communicators").  A program that initialises HIP through torch before it
+    imports the package runs with HIP's default 4: both ranks must refuse together, explained,
+    instead of hanging later in a cross-rank queue cycle."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "tests", "_hwq_early_init.py")]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
+    assert out.returncode != 0, out.stdout
+    for r in (0, 1):
+        assert f"rank {r}: effective queues 4" in out.stdout, out.stdout + out.stderr[-2000:]
+        assert f"rank {r}: refused: GPU_MAX_HW_QUEUES: rank(s) [0, 1] run with 4" in out.stdout, out.stdout
