@@ -142,6 +142,17 @@ def launch(args, argv) -> int:
     return max(codes)
 
 
+def _merge_transports(per_rank):
+    """RCCL channel connections per transport, summed over ranks (None: no RCCL in this run)."""
+    if all(t is None for t in per_rank):
+        return None
+    out = {}
+    for t in per_rank:
+        for k, v in (t or {}).items():
+            out[k] = out.get(k, 0) + v
+    return out
+
+
 # ----------------------------------------------------------------------------- one rank
 def run_rank(args) -> int:
     gpu = args.device == "gpu"
@@ -165,6 +176,17 @@ def run_rank(args) -> int:
     from mpi_jordan_crazy_acceleration_amd.runtime_env import configure_runtime_env
 
     configure_runtime_env()
+    # which transport RCCL connects the ranks with (P2P over xGMI, or sockets): its INFO log of the
+    # connection setup goes to a per-rank file, parsed after the warm-up (utils/rccl_log.py)
+    rccl_log = None
+    if gpu and (world > 1 or args.force_rccl):
+        import tempfile
+
+        from mpi_jordan_crazy_acceleration_amd.utils import rccl_log as _rl
+
+        path = os.path.join(tempfile.gettempdir(), f"gj_rccl_{os.getpid()}.log")
+        if _rl.enable(path):
+            rccl_log = path
     if args.bcast:
         os.environ["GJ_BCAST"] = args.bcast
     from datetime import timedelta
@@ -241,6 +263,10 @@ def run_rank(args) -> int:
             st = step()
             if st["status"] != 0:
                 return fail(f"solve failed with status {st['status']}")
+        if rccl_log:  # before the timed loop: every connection the solve uses is up after a warm-up
+            from mpi_jordan_crazy_acceleration_amd.utils.rccl_log import transports
+
+            print(f"bench.py: rank {rank}: RCCL transport {transports(rccl_log)}", file=sys.stderr, flush=True)
         barrier()
         t0 = time.perf_counter()
         stats = []
@@ -258,7 +284,12 @@ def run_rank(args) -> int:
         "host_wait_ms": max([s["host_wait_ms"] for s in stats] or [0.0]),
         "phases": stats[-1].get("phases") if stats else None,
         "policy": eng.policy,
+        "rccl_transport": None,
     }
+    if rccl_log:
+        from mpi_jordan_crazy_acceleration_amd.utils.rccl_log import transports
+
+        mine["rccl_transport"] = transports(rccl_log) or {}
     if dist.is_initialized():
         everyone = [None] * world
         dist.all_gather_object(everyone, mine)
@@ -321,6 +352,7 @@ def run_rank(args) -> int:
             "rank_solve_seconds_max": [round(x, 4) for x in per_rank_max],
             "host_wait_ms_max": round(max(e["host_wait_ms"] for e in everyone), 3),
             "host_wait_ms": round(st["host_wait_ms"], 3),
+            "rccl_transport": _merge_transports([e["rccl_transport"] for e in everyone]),
             "residual_inf": res,
             "residual_bound": bound,
             "check": check,

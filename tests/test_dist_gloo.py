@@ -94,3 +94,41 @@ def test_gloo_direct_bcast(monkeypatch):
     for rank, status, res, inv, corner in out:
         assert status == 0 and res < 1e-8, (status, res)
     assert np.abs(out[0][3] - ref).max() / np.abs(ref).max() < 1e-9
+
+
+def _bits_worker(rank, world, port, n, m, out):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from mpi_jordan_crazy_acceleration_amd.parallel import DistributedGaussJordan
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        gj = DistributedGaussJordan(n, m, host_threads=1)
+        gj.generate("random", 5)
+        assert gj.solve()["status"] == 0
+        inv = gj.gather_inverse()
+        if rank == 0:
+            np.save(out, inv)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_threaded_cli_and_process_ranks_same_bits(tmp_path, gj_bin):
+    """The in-process threaded runner (`gj -p 8`, one host thread per rank: csrc/solver/runner.cpp,
+    the same code path as `gj -p 8 --comm rccl` up to the transport) and one process per rank
+    (torch.distributed, the bench / torchrun path) must produce the same inverse, bit for bit."""
+    import subprocess
+
+    n, m, p = 333, 12, 8
+    binf = tmp_path / "inv.bin"
+    r = subprocess.run([gj_bin, "--device", "cpu", "--comm", "loopback", "-p", str(p), "--host-threads", "1",
+                        "--gen", "random", "--seed", "5", "--out", str(binf), str(n), str(m)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    threaded = np.fromfile(binf, dtype=np.float64).reshape(n, n)
+    out = str(tmp_path / "proc.npy")
+    mp.spawn(_bits_worker, args=(p, _free_port(), n, m, out), nprocs=p, join=True)
+    procs = np.load(out)
+    assert np.array_equal(threaded.view(np.int64), procs.view(np.int64))

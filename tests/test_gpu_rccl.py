@@ -27,6 +27,7 @@ def test_bench_under_torchrun_with_rccl():
     line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
     rep = json.loads(line)
     assert rep["status"] == 0 and rep["n_gpus"] == 1
+    assert isinstance(rep["rccl_transport"], dict)  # one rank: no channel connections to report
     assert rep["residual_inf"] < 1e-6
     assert rep["value"] > 0 and rep["ms_per_step"] > 0
 
@@ -62,6 +63,8 @@ def test_rccl_multi_rank_same_gpu(ranks, bcast):
     assert rep["residual_inf"] < 1e-6  # random 2048 x 2048: 2.7e-8
     assert abs(rep["residual_inf"] - one["residual_inf"]) <= 1e-3 * one["residual_inf"]
     assert len(rep["rank_solve_seconds_max"]) == ranks
+    # the rehearsal's ranks are separate RCCL "hosts": RCCL must have connected them over sockets
+    assert any(k.startswith("NET") for k in rep["rccl_transport"]), rep["rccl_transport"]
 
 
 def _cli(nproc, *args, timeout=300):
