@@ -25,6 +25,8 @@
 //   --depth D            elimination steps fused per trailing update (1..8; default: engine.hpp)
 //   --pivot block-min-inv-norm|partial   pivot rule (default: the reference's smallest ||inv||;
 //                        partial = block partial pivoting, one candidate inverse per rank and step)
+//   --pivot-growth G     partial pivoting: a candidate with ||inv||_inf * max|W| > G counts as
+//                        singular (default 1e8; 0 = off)
 //   --repeat R           time R solves, report the last (min also in --json)
 //   --out FILE           write the inverse (text, or .bin)
 //   --rhs ones|random|FILE  also solve A x = b (x = inv(A) b) and report ||A x - b||_inf
@@ -160,6 +162,7 @@ int main(int argc, char* argv[]) {
         else if (pv == "partial") cfg.solve.pivot = PivotRule::Partial;
         else return usage(argv[0]);
       }
+      else if (a == "--pivot-growth") cfg.solve.pivot_growth = std::atof(val("--pivot-growth"));
       else if (a == "--repeat") cfg.repeats = std::atoi(val("--repeat"));
       else if (a == "--out") out_file = val("--out");
       else if (a == "--rhs") cfg.rhs = val("--rhs");

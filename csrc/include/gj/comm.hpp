@@ -70,6 +70,10 @@ class Comm {
   void set_direct_bcast_min(size_t b) { direct_min_ = b; }
   const std::string& bcast_report() const { return bcast_report_; }
 
+  // The solver step the following collectives belong to (diagnostics; the single-GPU emulation
+  // ShadowComm synthesises its peers' pivot records from it).
+  virtual void set_step(int64_t t) { (void)t; }
+
   // Host-blocking helpers (once-per-run agreement: errors, timings, residual maxima).
   virtual void barrier(Device& dev) = 0;
   virtual double host_max(Device& dev, double v) = 0;

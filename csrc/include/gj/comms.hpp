@@ -193,6 +193,7 @@ class ShadowComm : public Comm {
   double host_max(Device&, double v) override { return v; }
   void host_allgather(Device& dev, const void* send, void* recv, size_t bytes) override;
   void reset() { step_ = 0; }
+  void set_step(int64_t t) override { step_ = t; }
   const CostModel& cost_model() const { return cm_; }
   double modelled_us() const { return modelled_us_; }  // total modelled transfer time issued
 

@@ -186,12 +186,13 @@ class Device {
   // common argmin (pivot_local) picks this rank's largest-magnitude candidate; its block alone is
   // then copied out (gather_candidate: sel = K-major m x m, ld m; -I for an invalid record),
   // inverted by block_inverse on a one-block layout, and commit_candidate stores that inverse in
-  // the candidate's slot of inv_t and clears rec->valid when the block is singular.
+  // the candidate's slot of inv_t and clears rec->valid when the block is singular or, growth > 0,
+  // when its growth estimate ||inv||_inf * max|W| (score1[0] * -rec->score) exceeds growth.
   virtual void candidate_maxabs(DType dt, const void* Lt, int64_t ldl, double* scores, int32_t* valid,
                                 const int32_t* used, const Layout& L, double thresh, int s) = 0;
   virtual void gather_candidate(DType dt, void* sel, const void* Lt, int64_t ldl, const PivotRec* rec,
                                 const Layout& L, int s) = 0;
-  virtual void commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1, PivotRec* rec,
+  virtual void commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1, const double* score1, double growth, PivotRec* rec,
                                 const Layout& L, int s) = 0;
   // Local argmin over this rank's candidates -> *out.
   virtual void pivot_local(const double* scores, const int32_t* valid, const int32_t* used,

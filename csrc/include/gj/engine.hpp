@@ -54,6 +54,10 @@ struct SolveOptions {
                             // else 4 (profiles/small_n_sweep.md, profiles/depth_pgt1.md)
   double eps = kDefaultEps;
   PivotRule pivot = PivotRule::MinInvNorm;
+  // PivotRule::Partial: a rank's candidate whose growth estimate ||inv(W)||_inf * max|W| exceeds
+  // this is treated as singular (another rank's, or the full MinInvNorm search, takes the step), so
+  // partial pivoting cannot silently accept a near-singular block.  <= 0: no guard.
+  double pivot_growth = 1e8;
   bool sync_debug = false;  // synchronise every stream after every phase (race screening)
   bool profile = false;     // per-phase device timers (HIP events) + roctx ranges
   double comm_timeout_s = 600;  // a host wait on a pivot longer than this is a peer failure

@@ -32,7 +32,7 @@ void candidate_maxabs(DType dt, const void* Lt, int64_t ldl, double* scores, int
                       const int32_t* used, const Layout& L, double thresh, hipStream_t s);
 void gather_candidate(DType dt, void* sel, const void* Lt, int64_t ldl, const PivotRec* rec, const Layout& L,
                       hipStream_t s);
-void commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1, PivotRec* rec,
+void commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1, const double* score1, double growth, PivotRec* rec,
                       const Layout& L, hipStream_t s);
 
 // blockinv.hip

@@ -321,9 +321,11 @@ void gather_candidate(DType dt, void* sel, const void* Lt, int64_t ldl, const Pi
 // valid only if that inverse exists (rec->valid &= valid1[0]).
 template <typename T>
 __global__ __launch_bounds__(256) void commit_candidate_kernel(T* __restrict__ inv_t, const T* __restrict__ inv1,
-                                                               const int32_t* __restrict__ valid1, int m,
-                                                               int64_t p, PivotRec* __restrict__ rec) {
-  const bool ok = rec->valid != 0 && valid1[0] != 0;
+                                                               const int32_t* __restrict__ valid1,
+                                                               const double* __restrict__ score1, double growth,
+                                                               int m, int64_t p, PivotRec* __restrict__ rec) {
+  // growth guard (SolveOptions::pivot_growth): ||inv(W)||_inf * max|W| above the bound = singular
+  const bool ok = rec->valid != 0 && valid1[0] != 0 && (growth <= 0.0 || score1[0] * -rec->score <= growth);
   const int64_t b = (int64_t)rec->phys / p;
   const int64_t total = (int64_t)m * m;
   if (ok)
@@ -334,15 +336,15 @@ __global__ __launch_bounds__(256) void commit_candidate_kernel(T* __restrict__ i
   if (blockIdx.x == 0 && threadIdx.x == 0 && !ok) rec->valid = 0;
 }
 
-void commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1, PivotRec* rec,
+void commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1, const double* score1, double growth, PivotRec* rec,
                       const Layout& L, hipStream_t s) {
   // one workgroup: rec is read by every thread before thread 0 may clear it
   if (dt == DType::F64)
     hipLaunchKernelGGL(commit_candidate_kernel<double>, dim3(1), dim3(256), 0, s, static_cast<double*>(inv_t),
-                       static_cast<const double*>(inv1), valid1, (int)L.m, L.p, rec);
+                       static_cast<const double*>(inv1), valid1, score1, growth, (int)L.m, L.p, rec);
   else
     hipLaunchKernelGGL(commit_candidate_kernel<float>, dim3(1), dim3(256), 0, s, static_cast<float*>(inv_t),
-                       static_cast<const float*>(inv1), valid1, (int)L.m, L.p, rec);
+                       static_cast<const float*>(inv1), valid1, score1, growth, (int)L.m, L.p, rec);
 }
 
 // ---------------------------------------------------------------- owner edits (one launch)

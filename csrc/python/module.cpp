@@ -403,8 +403,10 @@ PYBIND11_MODULE(_C, mod) {
   py::class_<PyEngine>(mod, "Engine")
       .def(py::init([](std::shared_ptr<Device> dev, std::shared_ptr<Comm> comm, int64_t n, int64_t m,
                        const std::string& dtype, int64_t chunk_cols, double eps, bool sync_debug,
-                       int depth, bool profile, double comm_timeout_s, const std::string& pivot) {
+                       int depth, bool profile, double comm_timeout_s, const std::string& pivot,
+                       double pivot_growth) {
              SolveOptions o;
+             o.pivot_growth = pivot_growth;
              o.dtype = parse_dtype(dtype);
              o.depth = depth;
              o.pivot = parse_pivot(pivot);
@@ -422,7 +424,7 @@ PYBIND11_MODULE(_C, mod) {
            py::arg("device"), py::arg("comm"), py::arg("n"), py::arg("m"), py::arg("dtype") = "fp64",
            py::arg("chunk_cols") = 0, py::arg("eps") = kDefaultEps, py::arg("sync_debug") = false,
            py::arg("depth") = 0, py::arg("profile") = false, py::arg("comm_timeout_s") = 600.0,
-           py::arg("pivot") = "block-min-inv-norm")
+           py::arg("pivot") = "block-min-inv-norm", py::arg("pivot_growth") = 1e8)
       .def_property_readonly("layout",
                              [](PyEngine& e) {
                                const Layout& L = e.eng->layout();
@@ -579,6 +581,7 @@ PYBIND11_MODULE(_C, mod) {
     if (d.contains("sync_debug")) c.solve.sync_debug = d["sync_debug"].cast<bool>();
     if (d.contains("depth")) c.solve.depth = d["depth"].cast<int>();
     if (d.contains("pivot")) c.solve.pivot = parse_pivot(d["pivot"].cast<std::string>());
+    if (d.contains("pivot_growth")) c.solve.pivot_growth = d["pivot_growth"].cast<double>();
     if (d.contains("profile")) c.solve.profile = d["profile"].cast<bool>();
     if (d.contains("rhs")) c.rhs = d["rhs"].cast<std::string>();
     if (d.contains("keep_solution")) c.keep_solution = d["keep_solution"].cast<bool>();

@@ -260,9 +260,9 @@ void AsyncHostDevice::gather_candidate(DType dt, void* sel, const void* Lt, int6
                                        const Layout& L, int s) {
   enqueue(s, [=] { inner_.gather_candidate(dt, sel, Lt, ldl, rec, L, s); });
 }
-void AsyncHostDevice::commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1,
+void AsyncHostDevice::commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1, const double* score1, double growth,
                                        PivotRec* rec, const Layout& L, int s) {
-  enqueue(s, [=] { inner_.commit_candidate(dt, inv_t, inv1, valid1, rec, L, s); });
+  enqueue(s, [=] { inner_.commit_candidate(dt, inv_t, inv1, valid1, score1, growth, rec, L, s); });
 }
 void AsyncHostDevice::pivot_local(const double* scores, const int32_t* valid, const int32_t* used,
                                   const int32_t* pos, const Layout& L, PivotRec* out, int s) {

@@ -268,9 +268,9 @@ void HipDevice::gather_candidate(DType dt, void* sel, const void* Lt, int64_t ld
   kern::gather_candidate(dt, sel, Lt, ldl, rec, L, hs(streams_[s]));
   check_launch();
 }
-void HipDevice::commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1, PivotRec* rec,
+void HipDevice::commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1, const double* score1, double growth, PivotRec* rec,
                                  const Layout& L, int s) {
-  kern::commit_candidate(dt, inv_t, inv1, valid1, rec, L, hs(streams_[s]));
+  kern::commit_candidate(dt, inv_t, inv1, valid1, score1, growth, rec, L, hs(streams_[s]));
   check_launch();
 }
 void HipDevice::pivot_local(const double* scores, const int32_t* valid, const int32_t* used,

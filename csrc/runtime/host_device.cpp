@@ -294,9 +294,10 @@ void HostDevice::gather_candidate(DType dt, void* sel, const void* Lt, int64_t l
     }
 }
 
-void HostDevice::commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1, PivotRec* rec,
+void HostDevice::commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1, const double* score1, double growth, PivotRec* rec,
                                   const Layout& L, int) {
-  if (!rec->valid || !valid1[0]) {
+  // growth guard: ||inv(W)||_inf * max|W| (score1 * -rec->score) above the bound counts as singular
+  if (!rec->valid || !valid1[0] || (growth > 0 && !(score1[0] * -rec->score <= growth))) {
     rec->valid = 0;
     return;
   }

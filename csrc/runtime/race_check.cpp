@@ -555,13 +555,14 @@ void RaceCheckDevice::gather_candidate(DType dt, void* sel, const void* Lt, int6
          W(span(sel, L.m * L.m * es), "sel")});
   inner_->gather_candidate(dt, sel, Lt, ldl, rec, L, s);
 }
-void RaceCheckDevice::commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1,
+void RaceCheckDevice::commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* valid1, const double* score1, double growth,
                                        PivotRec* rec, const Layout& L, int s) {
   const int64_t es = (int64_t)dtype_size(dt);
   check(s, "commit_candidate",
-        {R(span(inv1, L.m * L.m * es), "inv1"), R(span(valid1, 4), "valid1"), W(span(rec, sizeof(PivotRec)), "rec"),
+        {R(span(inv1, L.m * L.m * es), "inv1"), R(span(valid1, 4), "valid1"), R(span(score1, 8), "score1"),
+         W(span(rec, sizeof(PivotRec)), "rec"),
          W(span(inv_t, L.nblk * L.m * L.m * es), "inv")});
-  inner_->commit_candidate(dt, inv_t, inv1, valid1, rec, L, s);
+  inner_->commit_candidate(dt, inv_t, inv1, valid1, score1, growth, rec, L, s);
 }
 void RaceCheckDevice::pivot_local(const double* scores, const int32_t* valid, const int32_t* used, const int32_t* pos,
                                   const Layout& L, PivotRec* out, int s) {

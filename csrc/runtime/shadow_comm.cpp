@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 
 #include "gj/comms.hpp"
 #include "gj/pivot.hpp"
@@ -48,7 +49,9 @@ void ShadowComm::allgather(Device& dev, const void* send, void* recv, size_t byt
     for (int q = 1; q < p_; ++q) dev.copy(static_cast<char*>(recv) + q * bytes, send, bytes, s);
     return;
   }
-  const int64_t t = step_++;
+  // the engine's step (Comm::set_step): a --pivot partial fallback's second exchange of a step
+  // must see the same synthetic winner as its first
+  const int64_t t = step_;
   const size_t slot = (size_t)p_ * bytes;
   if (!pin_ || pin_hip_ != dev.on_gpu() || pin_bytes_ < kSlots * slot) {
     dev.sync_all();
@@ -72,7 +75,9 @@ void ShadowComm::allgather(Device& dev, const void* send, void* recv, size_t byt
   for (int q = 1; q < p_; ++q) recs[q] = pivot_invalid();
   const int q = (int)(t % p_);
   if (q != 0) {
-    recs[q].score = 0.0;  // strictly better than any real ||inv||
+    // strictly better than any real record under both rules (MinInvNorm scores ||inv|| >= 0,
+    // Partial scores -max|W| < 0)
+    recs[q].score = -std::numeric_limits<double>::max();
     recs[q].logical = (int32_t)t;
     recs[q].phys = (int32_t)t;
     recs[q].valid = 1;

@@ -562,7 +562,7 @@ void Engine::select(int64_t t, const void* Lt, bool full) {
     dev_.set_block_inverse_hint(bi_hint_);
     dev_.block_inverse(opt_.dtype, sel_, L_.m, inv1_, score1_, valid1_, used1_, L1_, thresh, 1, S_SIDE);
     dev_.set_block_inverse_hint(-1);
-    dev_.commit_candidate(opt_.dtype, inv_, inv1_, valid1_, myrec_, L_, S_SIDE);
+    dev_.commit_candidate(opt_.dtype, inv_, inv1_, valid1_, score1_, opt_.pivot_growth, myrec_, L_, S_SIDE);
     prof_end(PH_PIVOT, pe, S_SIDE);
   } else {
     // The selection runs in the candidate-inverse launch's last workgroup where the kernel family
@@ -613,6 +613,7 @@ void Engine::select(int64_t t, const void* Lt, bool full) {
     return;
   }
   pe = prof_begin(S_SIDE);
+  comm_.set_step(t);
   if (L_.p > 1) comm_.allgather(dev_, myrec_, recs_, sizeof(PivotRec), S_SIDE);
   dev_.host_access(&piv_host_[par].step, sizeof(int32_t), true);
   piv_host_[par].step = -1;

@@ -91,3 +91,25 @@ def test_partial_on_gpu(n, m, p):
 def test_partial_fallback_on_gpu():
     rep = gj.GaussJordan(block_size=64, ranks=2, device="gpu", comm="async", pivot="partial").run(1024, gen="absdiff")
     assert rep["status"] == 0 and rep["stats"]["pivot_fallbacks"] > 0 and rep["residual"] < 1e-6
+
+
+@pytest.mark.parametrize("p", [1, 2])
+def test_partial_growth_guard(p):
+    """A candidate with the column's largest entries but nearly singular (growth estimate
+    ||inv(W)||_inf max|W| ~ 1e11, above the default bound 1e8) must not be accepted by partial
+    pivoting: with the guard the step takes another rank's block or the full search; without it
+    (pivot_growth = 0) the near-singular pivot is taken (a silently low-accuracy inverse)."""
+    m, Nr = 4, 8
+    n = m * Nr
+    rng = np.random.default_rng(3)
+    A = rng.uniform(-1, 1, (n, n)) + 2 * np.eye(n)
+    u, v = rng.uniform(0.5, 1, m), rng.uniform(0.5, 1, m)
+    A[2 * m:3 * m, :m] = 100.0 * np.outer(u, v) + 1e-9 * np.eye(m)  # block row 2: big, rank 1 + 1e-9 I
+    guarded = gj.GaussJordan(block_size=m, ranks=p, device="cpu", pivot="partial").run(n, input=A, keep_inverse=True)
+    assert guarded["status"] == 0 and guarded["stats"]["pivots"][0] != 2
+    off = gj.GaussJordan(block_size=m, ranks=p, device="cpu", pivot="partial", extra={"pivot_growth": 0.0}).run(
+        n, input=A, keep_inverse=True)
+    assert off["status"] == 0 and off["stats"]["pivots"][0] == 2
+    ref = np.linalg.inv(A)
+    err = lambda r: np.abs(r["inverse"] - ref).max() / np.abs(ref).max()  # noqa: E731
+    assert err(guarded) < 1e-10 and err(guarded) < err(off)

@@ -53,3 +53,20 @@ def test_p2p_cost_is_per_link(monkeypatch):
     modelled = C.shadow_modelled_us(comm) - before
     slice_us = (nbytes / (p - 1)) / (bw * 1e3)
     assert modelled == pytest.approx(2 * slice_us, rel=0.02)
+
+
+@pytest.mark.parametrize("pivot", ["block-min-inv-norm", "partial"])
+def test_shadow_synthetic_peers_win_under_both_rules(pivot):
+    """The emulated peers' records must win at every step t with t % p != 0 under either pivot rule
+    (Partial scores are -max|W| < 0, so a synthetic score of 0 would lose to rank 0's own block; ADVICE
+    r3), and the step comes from the engine (a partial fallback's second exchange repeats a step)."""
+    C = load_native()
+    p, n, m = 4, 512, 32
+    comm = C.shadow_comm(p, 0.0, 0.0, 16)
+    eng = C.Engine(C.host_device(2), comm, n, m, "fp64", pivot=pivot)
+    eng.generate("random", 1)
+    st = eng.solve()
+    assert st["status"] == 0
+    piv = st["pivots"]
+    assert all(piv[t] == t for t in range(len(piv)) if t % p != 0), piv
+    assert all(piv[t] % p == 0 for t in range(len(piv)) if t % p == 0), piv
