@@ -81,8 +81,10 @@ class AsyncHostDevice : public Device {
   void pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos, int32_t* phys_at,
                     int32_t* used, int32_t* seq, PivotResult* out, PivotResult* host_out,
                     int s) override;
-  void owner_edits(DType dt, void* At, int64_t ldl, int64_t row0, int64_t j, int64_t m, void* lrow,
-                   void* ht, const void* inv_blk, int s) override;
+  void owner_edits(DType dt, void* At, int64_t ldl, const int32_t* phys, int64_t p, int64_t k, int64_t j,
+                   int64_t m, void* lrow, void* ht, const void* inv, int s) override;
+  void take_rows(DType dt, void* dst, int64_t ldd, void* X, int64_t ldx, const int32_t* phys, int64_t p, int64_t k,
+                 int64_t col0, int64_t w, int64_t m, int s) override;
   void h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, int s) override;
   void gemm(DType dt, GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const void* A,
             int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int s,

@@ -212,14 +212,22 @@ class Device {
     pivot_local(scores, valid, used, pos, L, rec, s);
     pivot_global(rec, 1, t, pos, phys_at, used, seq, out, host_out, s);
   }
-  // Owner-side edits of a pivot step, fused (one launch): for the pivot's local block row b0 (rows
-  // row0 .. row0+m-1 of the K-major multiplier panel At, ld ldl) save the multipliers of the panel's
-  // earlier steps, lrow[k*m + c] = At[k*ldl + row0 + c] for k < j*m, then set those rows of At to
-  // [0 .. 0 | I] over the first (j+1)*m K-rows (identity in segment j), and copy the m x m block
-  // inverse: ht[e] = inv_blk[e], e < m*m.
-  virtual void owner_edits(DType dt, void* At, int64_t ldl, int64_t row0, int64_t j, int64_t m,
-                           void* lrow, void* ht, const void* inv_blk, int s) = 0;
-  // R[i*ldr + j] = H[i][j] = Ht[j*m + i]   (the pivot column block of the broadcast row).
+  // Owner-side edits of a pivot step, fused (one launch).  The pivot is read on the device: g =
+  // *phys (the step's entry of the pivot sequence, written by the selection), and the launch does
+  // nothing unless g % p == k (this rank owns it), so the host can enqueue it before it has seen
+  // the pivot.  For the pivot's local block row b = g / p (rows row0 = b m .. of the K-major
+  // multiplier panel At, ld ldl): save the multipliers of the panel's earlier steps,
+  // lrow[kk*m + c] = At[kk*ldl + row0 + c] for kk < j*m, set those rows of At to [0 .. 0 | I] over
+  // the first (j+1)*m K-rows (identity in segment j), and copy the block's inverse:
+  // ht[e] = inv[b*m*m + e], e < m*m.
+  virtual void owner_edits(DType dt, void* At, int64_t ldl, const int32_t* phys, int64_t p, int64_t k,
+                           int64_t j, int64_t m, void* lrow, void* ht, const void* inv, int s) = 0;
+  // Take the pivot row's piece (device-addressed like owner_edits): for g = *phys owned here (else
+  // nothing), local rows row0 = (g / p) m .. + m:  dst[r*ldd + c] = X[(row0 + r)*ldx + col0 + c],
+  // then X[row0 + r][col0 + c] = 0, for r < m, c < w.  The panel's later columns of a pivot row
+  // enter the next column updates as 0 (the sweep's zero-row rule) without a zero-row mask.
+  virtual void take_rows(DType dt, void* dst, int64_t ldd, void* X, int64_t ldx, const int32_t* phys, int64_t p,
+                         int64_t k, int64_t col0, int64_t w, int64_t m, int s) = 0;
   virtual void h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, int s) = 0;
   virtual void gemm(DType dt, GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const void* A,
                     int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int s,

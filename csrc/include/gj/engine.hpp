@@ -174,18 +174,27 @@ class Engine {
 
  private:
   static constexpr int kMaxDepth = GemmExtra::kMaxZeroRows;
+  // pinned pivot-result slots: one per step of a panel in flight (the host-free chain of one rank
+  // enqueues a whole panel's steps before it reads any result)
+  static constexpr int kPivSlots = 2 * kMaxDepth;
+  static int hslot(int64_t t) { return (int)(t % kPivSlots); }
+  // One rank and the reference pivot rule: the pivot chain is enqueued a panel at a time, every
+  // owner-side launch reading the pivot from device memory, the host reading the results after it
+  // (no host round trip per step).  Elsewhere the host needs each root before it can broadcast.
+  bool host_free_chain() const { return L_.p == 1 && opt_.pivot == PivotRule::MinInvNorm && !opt_.sync_debug; }
   // 0 = ok, 1 = the work space does not fit, 2 = the matrix panels do not fit (why: the reason)
   int alloc_buffers(std::string& why);
   void alloc_work(int64_t wmax);
   void free_work();     // everything but the matrix panels
   void label_work();    // buffer names for schedule-check reports
   void free_buffers();
-  // Pivot search for step t on the multiplier segment Lt (SIDE stream); result -> piv_host_[t&1].
+  // Pivot search for step t on the multiplier segment Lt (SIDE stream); result -> piv_host_[hslot(t)].
   void select(int64_t t, const void* Lt, bool full = false);
   // Panel factorisation (pivot searches of its q steps, panel pieces, then the chunk pipeline of
   // the normalised pivot rows).  Returns false when the matrix is singular.
   void begin_panel(int64_t v);
   bool factor_panel(int64_t v, SolveStats& st, double& host_wait);
+  bool await_step(int64_t v, int64_t j, SolveStats& st, double& host_wait, PivotResult& r);
   void lookahead_rows(int64_t v, bool wait_main);
   void chunk_pipeline(int64_t v, bool wait_main);
   void lookahead_update(int64_t u);
@@ -281,7 +290,7 @@ class Engine {
   int64_t live_ = 0;                   // local block rows not yet used as a pivot row (candidates)
 
   // events
-  int ev_L_ = -1, ev_main_ = -1, ev_sel_[2] = {-1, -1}, ev_edit_[2] = {-1, -1};
+  int ev_L_ = -1, ev_main_ = -1, ev_edit_[2] = {-1, -1};
   int ev_pp_[2][kMaxDepth] = {};
   int ev_la_[2] = {-1, -1};            // LA_[par] formed and broadcast (COMM)
   int ev_cp_[2] = {-1, -1};            // chunk pass of a panel of that parity done (COMM)

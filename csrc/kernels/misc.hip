@@ -348,35 +348,69 @@ void commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* va
 }
 
 // ---------------------------------------------------------------- owner edits (one launch)
+// The pivot comes from device memory (the step's pivot-sequence entry): the launch can be enqueued
+// before the host has seen the pivot, and is a no-op on ranks that do not own it.
 template <typename T>
-__global__ __launch_bounds__(256) void owner_edits_kernel(T* At, int64_t ldl, int64_t row0, int64_t j,
-                                                          int64_t m, T* lrow, T* ht, const T* inv_blk) {
+__global__ __launch_bounds__(256) void owner_edits_kernel(T* At, int64_t ldl, const int32_t* __restrict__ phys,
+                                                          int64_t p, int64_t k, int64_t j, int64_t m, T* lrow, T* ht,
+                                                          const T* inv) {
+  const int64_t g = *phys;
+  if (g < 0 || g % p != k) return;
+  const int64_t b = g / p, row0 = b * m;
+  const T* inv_blk = inv + b * m * m;
   const int64_t nrow = (j + 1) * m, total = nrow * m;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total + m * m;
        e += (int64_t)gridDim.x * blockDim.x) {
     if (e < total) {
-      const int64_t k = e / m, c = e - k * m;
-      T* x = At + k * ldl + row0 + c;
-      if (k < j * m) lrow[k * m + c] = *x;
-      *x = (k - j * m == c) ? T(1) : T(0);
+      const int64_t kk = e / m, c = e - kk * m;
+      T* x = At + kk * ldl + row0 + c;
+      if (kk < j * m) lrow[kk * m + c] = *x;
+      *x = (kk - j * m == c) ? T(1) : T(0);
     } else {
       ht[e - total] = inv_blk[e - total];
     }
   }
 }
 
-void owner_edits(DType dt, void* At, int64_t ldl, int64_t row0, int64_t j, int64_t m, void* lrow,
-                 void* ht, const void* inv_blk, hipStream_t s) {
+void owner_edits(DType dt, void* At, int64_t ldl, const int32_t* phys, int64_t p, int64_t k, int64_t j,
+                 int64_t m, void* lrow, void* ht, const void* inv, hipStream_t s) {
   const int64_t work = (j + 2) * m * m;
   const unsigned grid = grid_for(work, 256, 256);
   if (dt == DType::F64)
-    hipLaunchKernelGGL(owner_edits_kernel<double>, dim3(grid), dim3(256), 0, s, static_cast<double*>(At),
-                       ldl, row0, j, m, static_cast<double*>(lrow), static_cast<double*>(ht),
-                       static_cast<const double*>(inv_blk));
+    hipLaunchKernelGGL(owner_edits_kernel<double>, dim3(grid), dim3(256), 0, s, static_cast<double*>(At), ldl, phys,
+                       p, k, j, m, static_cast<double*>(lrow), static_cast<double*>(ht),
+                       static_cast<const double*>(inv));
   else
-    hipLaunchKernelGGL(owner_edits_kernel<float>, dim3(grid), dim3(256), 0, s, static_cast<float*>(At),
-                       ldl, row0, j, m, static_cast<float*>(lrow), static_cast<float*>(ht),
-                       static_cast<const float*>(inv_blk));
+    hipLaunchKernelGGL(owner_edits_kernel<float>, dim3(grid), dim3(256), 0, s, static_cast<float*>(At), ldl, phys, p,
+                       k, j, m, static_cast<float*>(lrow), static_cast<float*>(ht), static_cast<const float*>(inv));
+}
+
+// The pivot row's piece of the panel's later columns, moved out (copied, then zeroed in X).
+template <typename T>
+__global__ __launch_bounds__(256) void take_rows_kernel(T* dst, int64_t ldd, T* X, int64_t ldx,
+                                                        const int32_t* __restrict__ phys, int64_t p, int64_t k,
+                                                        int64_t col0, int64_t w, int64_t m) {
+  const int64_t g = *phys;
+  if (g < 0 || g % p != k) return;
+  const int64_t row0 = (g / p) * m, total = m * w;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / w, c = e - r * w;
+    T* x = X + (row0 + r) * ldx + col0 + c;
+    dst[r * ldd + c] = *x;
+    *x = T(0);
+  }
+}
+
+void take_rows(DType dt, void* dst, int64_t ldd, void* X, int64_t ldx, const int32_t* phys, int64_t p, int64_t k,
+               int64_t col0, int64_t w, int64_t m, hipStream_t s) {
+  if (w <= 0 || m <= 0) return;
+  const unsigned grid = grid_for(m * w, 256, 256);
+  if (dt == DType::F64)
+    hipLaunchKernelGGL(take_rows_kernel<double>, dim3(grid), dim3(256), 0, s, static_cast<double*>(dst), ldd,
+                       static_cast<double*>(X), ldx, phys, p, k, col0, w, m);
+  else
+    hipLaunchKernelGGL(take_rows_kernel<float>, dim3(grid), dim3(256), 0, s, static_cast<float*>(dst), ldd,
+                       static_cast<float*>(X), ldx, phys, p, k, col0, w, m);
 }
 
 // ---------------------------------------------------------------- permute_blocks

@@ -288,9 +288,13 @@ void AsyncHostDevice::pivot_global_now(const PivotRec* recs, int32_t p, int32_t 
     *reinterpret_cast<volatile int32_t*>(&host_out->step) = step;
   }
 }
-void AsyncHostDevice::owner_edits(DType dt, void* At, int64_t ldl, int64_t row0, int64_t j, int64_t m,
-                                  void* lrow, void* ht, const void* inv_blk, int s) {
-  enqueue(s, [=] { inner_.owner_edits(dt, At, ldl, row0, j, m, lrow, ht, inv_blk, s); });
+void AsyncHostDevice::owner_edits(DType dt, void* At, int64_t ldl, const int32_t* phys, int64_t p, int64_t k,
+                                  int64_t j, int64_t m, void* lrow, void* ht, const void* inv, int s) {
+  enqueue(s, [=] { inner_.owner_edits(dt, At, ldl, phys, p, k, j, m, lrow, ht, inv, s); });
+}
+void AsyncHostDevice::take_rows(DType dt, void* dst, int64_t ldd, void* X, int64_t ldx, const int32_t* phys,
+                                int64_t p, int64_t k, int64_t col0, int64_t w, int64_t m, int s) {
+  enqueue(s, [=] { inner_.take_rows(dt, dst, ldd, X, ldx, phys, p, k, col0, w, m, s); });
 }
 void AsyncHostDevice::h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, int s) {
   enqueue(s, [=] { inner_.h_block(dt, R, ldr, Ht, m, s); });

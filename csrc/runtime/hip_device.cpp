@@ -292,9 +292,14 @@ void HipDevice::pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t
   kern::pivot_global(recs, p, t, pos, phys_at, used, seq, out, host_out, hs(streams_[s]));
   check_launch();
 }
-void HipDevice::owner_edits(DType dt, void* At, int64_t ldl, int64_t row0, int64_t j, int64_t m,
-                            void* lrow, void* ht, const void* inv_blk, int s) {
-  kern::owner_edits(dt, At, ldl, row0, j, m, lrow, ht, inv_blk, hs(streams_[s]));
+void HipDevice::owner_edits(DType dt, void* At, int64_t ldl, const int32_t* phys, int64_t p, int64_t k, int64_t j,
+                            int64_t m, void* lrow, void* ht, const void* inv, int s) {
+  kern::owner_edits(dt, At, ldl, phys, p, k, j, m, lrow, ht, inv, hs(streams_[s]));
+  check_launch();
+}
+void HipDevice::take_rows(DType dt, void* dst, int64_t ldd, void* X, int64_t ldx, const int32_t* phys, int64_t p,
+                          int64_t k, int64_t col0, int64_t w, int64_t m, int s) {
+  kern::take_rows(dt, dst, ldd, X, ldx, phys, p, k, col0, w, m, hs(streams_[s]));
   check_launch();
 }
 void HipDevice::h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, int s) {

@@ -347,24 +347,38 @@ void HostDevice::pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_
   if (host_out) *host_out = r;
 }
 
-void HostDevice::owner_edits(DType dt, void* At, int64_t ldl, int64_t row0, int64_t j, int64_t m,
-                             void* lrow, void* ht, const void* inv_blk, int) {
-  auto run = [&](auto* a, auto* lr, auto* h, const auto* inv) {
+void HostDevice::owner_edits(DType dt, void* At, int64_t ldl, const int32_t* phys, int64_t p, int64_t k,
+                             int64_t j, int64_t m, void* lrow, void* ht, const void* inv, int) {
+  const int64_t g = *phys;
+  if (g < 0 || g % p != k) return;
+  const int64_t row0 = (g / p) * m;
+  auto run = [&](auto* a, auto* lr, auto* h, const auto* iv) {
     using T = std::remove_pointer_t<decltype(a)>;
-    for (int64_t k = 0; k < (j + 1) * m; ++k)
+    for (int64_t kk = 0; kk < (j + 1) * m; ++kk)
       for (int64_t c = 0; c < m; ++c) {
-        T& x = a[k * ldl + row0 + c];
-        if (k < j * m) lr[k * m + c] = x;
-        x = (k - j * m == c) ? T(1) : T(0);
+        T& x = a[kk * ldl + row0 + c];
+        if (kk < j * m) lr[kk * m + c] = x;
+        x = (kk - j * m == c) ? T(1) : T(0);
       }
-    for (int64_t e = 0; e < m * m; ++e) h[e] = inv[e];
+    for (int64_t e = 0; e < m * m; ++e) h[e] = iv[(g / p) * m * m + e];
   };
   if (dt == DType::F64)
-    run(static_cast<double*>(At), static_cast<double*>(lrow), static_cast<double*>(ht),
-        static_cast<const double*>(inv_blk));
+    run(static_cast<double*>(At), static_cast<double*>(lrow), static_cast<double*>(ht), static_cast<const double*>(inv));
   else
-    run(static_cast<float*>(At), static_cast<float*>(lrow), static_cast<float*>(ht),
-        static_cast<const float*>(inv_blk));
+    run(static_cast<float*>(At), static_cast<float*>(lrow), static_cast<float*>(ht), static_cast<const float*>(inv));
+}
+
+void HostDevice::take_rows(DType dt, void* dst, int64_t ldd, void* X, int64_t ldx, const int32_t* phys, int64_t p,
+                           int64_t k, int64_t col0, int64_t w, int64_t m, int) {
+  const int64_t g = *phys;
+  if (g < 0 || g % p != k || w <= 0) return;
+  const size_t es = dtype_size(dt);
+  const int64_t row0 = (g / p) * m;
+  for (int64_t r = 0; r < m; ++r) {
+    char* src = static_cast<char*>(X) + ((row0 + r) * ldx + col0) * (int64_t)es;
+    std::memcpy(static_cast<char*>(dst) + r * ldd * (int64_t)es, src, (size_t)w * es);
+    std::memset(src, 0, (size_t)w * es);
+  }
 }
 
 void HostDevice::h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, int) {

@@ -132,14 +132,34 @@ void HbChecker::report(const Alloc& al, const Rec& old, const Access& acc, uint3
   reports_.push_back(o.str());
 }
 
-void HbChecker::check_and_record(int a, const Clock& c, uint32_t opid, const std::vector<Access>& acc) {
+void HbChecker::check_and_record(int a, const Clock& c, uint32_t opid, const std::vector<Access>& acc_in) {
+  std::vector<Access> acc = acc_in;
   std::vector<Alloc*> where_(acc.size(), nullptr);
   for (size_t i = 0; i < acc.size(); ++i) {
-    const Access& x = acc[i];
-    if (empty(x.r)) continue;
+    Access& x = acc[i];
+    if (x.r.base == nullptr) continue;
     Alloc* al = find(x.r.base);
     where_[i] = al;
     if (!al) continue;  // untracked memory
+    // extents the op could not know (device-addressed rows): to the end of the allocation
+    uintptr_t abase = 0;
+    for (auto it = allocs_.upper_bound((uintptr_t)x.r.base); it != allocs_.begin();) {
+      --it;
+      abase = it->first;
+      break;
+    }
+    const int64_t left = (int64_t)(abase + al->bytes) - (int64_t)(uintptr_t)x.r.base;
+    if (x.r.width < 0) {
+      x.r.width = left;
+      x.r.pitch = left;
+      x.r.height = 1;
+    } else if (x.r.height < 0) {
+      x.r.height = x.r.pitch > 0 && left >= x.r.width ? (left - x.r.width) / x.r.pitch + 1 : 1;
+    }
+    if (empty(x.r)) {
+      where_[i] = nullptr;
+      continue;
+    }
     for (const Rec& r : al->recs) {
       if (!(r.write || x.write)) continue;
       if (at(c, r.agent) >= r.epoch) continue;  // ordered before this op
@@ -597,14 +617,25 @@ void RaceCheckDevice::pivot_select_single(const double* scores, const int32_t* v
   inner_->pivot_select_single(scores, valid, L, t, pos, phys_at, used, seq, rec, out, host_out, s);
   if (host_out) hb_->release_point(host_out, id_, s);
 }
-void RaceCheckDevice::owner_edits(DType dt, void* At, int64_t ldl, int64_t row0, int64_t j, int64_t m, void* lrow,
-                                  void* ht, const void* inv_blk, int s) {
+void RaceCheckDevice::owner_edits(DType dt, void* At, int64_t ldl, const int32_t* phys, int64_t p, int64_t k,
+                                  int64_t j, int64_t m, void* lrow, void* ht, const void* inv, int s) {
   const int64_t es = (int64_t)dtype_size(dt);
-  std::vector<Acc> a{W(rect(static_cast<char*>(At) + row0 * es, ldl, m, (j + 1) * m, es), "At rows"),
-                     W(span(ht, m * m * es), "Ht"), R(span(inv_blk, m * m * es), "inv")};
+  // the pivot's rows are chosen on the device: every row of the first (j + 1) m K-rows, every block
+  // of the inverses (height / width -1: to the end of the allocation)
+  std::vector<Acc> a{R(span(phys, 4), "phys"), W(rect(At, ldl, ldl, (j + 1) * m, es), "At rows"),
+                     W(span(ht, m * m * es), "Ht"), R(MemRegion{static_cast<const char*>(inv), -1, -1, 1}, "inv")};
   if (j > 0) a.push_back(W(span(lrow, j * m * m * es), "Lrow"));
   check(s, "owner_edits", a);
-  inner_->owner_edits(dt, At, ldl, row0, j, m, lrow, ht, inv_blk, s);
+  inner_->owner_edits(dt, At, ldl, phys, p, k, j, m, lrow, ht, inv, s);
+}
+void RaceCheckDevice::take_rows(DType dt, void* dst, int64_t ldd, void* X, int64_t ldx, const int32_t* phys,
+                                int64_t p, int64_t k, int64_t col0, int64_t w, int64_t m, int s) {
+  const int64_t es = (int64_t)dtype_size(dt);
+  MemRegion xr = rect(static_cast<char*>(X) + col0 * es, ldx, w, 1, es);
+  xr.pitch = ldx * es;
+  xr.height = -1;  // rows of the pivot chosen on the device: the column range of every row
+  check(s, "take_rows", {R(span(phys, 4), "phys"), W(xr, "X piece"), W(rect(dst, ldd, w, m, es), "dst")});
+  inner_->take_rows(dt, dst, ldd, X, ldx, phys, p, k, col0, w, m, s);
 }
 void RaceCheckDevice::h_block(DType dt, void* Rp, int64_t ldr, const void* Ht, int64_t m, int s) {
   const int64_t es = (int64_t)dtype_size(dt);

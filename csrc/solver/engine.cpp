@@ -306,7 +306,7 @@ void Engine::alloc_work(int64_t wmax) {
   dscratch_ = static_cast<double*>(dev_.alloc(sizeof(double) * 64));
   ihost_len_ = std::max<int64_t>(L_.Nr, 16) * 2 + 16;
   iscratch_ = static_cast<int32_t*>(dev_.alloc(sizeof(int32_t) * ihost_len_));
-  piv_host_ = static_cast<PivotResult*>(dev_.alloc_pinned_coherent(sizeof(PivotResult) * 2));
+  piv_host_ = static_cast<PivotResult*>(dev_.alloc_pinned_coherent(sizeof(PivotResult) * kPivSlots));
   ihost_ = static_cast<int32_t*>(dev_.alloc_pinned(sizeof(int32_t) * ihost_len_));
   dhost_ = static_cast<double*>(dev_.alloc_pinned(sizeof(double) * 64));
   label_work();
@@ -315,7 +315,6 @@ void Engine::alloc_work(int64_t wmax) {
   ev_L_ = dev_.create_event();
   ev_main_ = dev_.create_event();
   for (int i = 0; i < 2; ++i) {
-    ev_sel_[i] = dev_.create_event();
     ev_edit_[i] = dev_.create_event();
     for (int j = 0; j < kMaxDepth; ++j) ev_pp_[i][j] = dev_.create_event();
     ev_la_[i] = dev_.create_event();
@@ -550,7 +549,9 @@ double Engine::norm_inf() {
 
 // ---------------------------------------------------------------- pivot search (SIDE stream)
 void Engine::select(int64_t t, const void* Lt, bool full) {
-  const int par = (int)(t & 1);
+  const int par = hslot(t);
+  // unused local blocks: exact at p = 1 (every step uses one), else counted as pivots arrive
+  const int64_t nlive = L_.p == 1 ? L_.nblk - t : live_;
   const double thresh = opt_.eps * norm_a_;
   Range rg(opt_.profile, "gj:select");
   int pe = prof_begin(S_SIDE);
@@ -590,9 +591,9 @@ void Engine::select(int64_t t, const void* Lt, bool full) {
         sa.out = piv_dev_;
         sa.host_out = &piv_host_[par];
       }
-      fused = dev_.block_inverse_select(opt_.dtype, Lt, L_.rows, inv_, scores_, valid_, used_, L_, thresh, live_, sa,
+      fused = dev_.block_inverse_select(opt_.dtype, Lt, L_.rows, inv_, scores_, valid_, used_, L_, thresh, nlive, sa,
                                         S_SIDE);
-      if (!fused) dev_.block_inverse(opt_.dtype, Lt, L_.rows, inv_, scores_, valid_, used_, L_, thresh, live_, S_SIDE);
+      if (!fused) dev_.block_inverse(opt_.dtype, Lt, L_.rows, inv_, scores_, valid_, used_, L_, thresh, nlive, S_SIDE);
       dev_.set_block_inverse_hint(-1);
     }
     if (L_.p == 1) {
@@ -600,7 +601,6 @@ void Engine::select(int64_t t, const void* Lt, bool full) {
         dev_.pivot_select_single(scores_, valid_, L_, (int32_t)t, pos_, phys_at_, used_, seq_, myrec_,
                                  piv_dev_, &piv_host_[par], S_SIDE);
       prof_end(PH_PIVOT, pe, S_SIDE);
-      dev_.record(ev_sel_[par], S_SIDE);
       dbg_sync();
       return;
     }
@@ -620,7 +620,6 @@ void Engine::select(int64_t t, const void* Lt, bool full) {
   dev_.pivot_global(L_.p > 1 ? recs_ : myrec_, (int32_t)L_.p, (int32_t)t, pos_, phys_at_, used_, seq_, piv_dev_,
                     &piv_host_[par], S_SIDE);
   prof_end(PH_EXCHANGE, pe, S_SIDE);
-  dev_.record(ev_sel_[par], S_SIDE);
   dbg_sync();
 }
 
@@ -648,26 +647,30 @@ void Engine::begin_panel(int64_t v) {
 // Pivot searches of panel v (the first one already enqueued by begin_panel); every later column
 // of the panel is brought up to date on the SIDE stream from the broadcast panel pieces.  For
 // every step: owner edits (Lrow save, H, multiplier rows -> [0..I]), then the panel piece
-// PP_t = H_t X^(t)[s_t, panel columns] and its (small) broadcast.
+// PP_t = H_t X^(t)[s_t, panel columns] and its (small) broadcast.  The owner-side launches read
+// the pivot from device memory (seq_[t]); with host_free_chain() the host enqueues all q steps and
+// reads their results afterwards, otherwise it waits for each pivot (it needs the broadcast root).
 bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
   const int par = (int)(v & 1);
   const int64_t m = L_.m, rows = L_.rows, npad = L_.npad, dm = (int64_t)d_ * m;
   const int64_t t0 = panel_t0(v), q = panel_q(v);
   const size_t es = esz();
+  const bool ahead = host_free_chain();
   for (int64_t j = 0; j < q; ++j) {
     const int64_t t = t0 + j;
     cur_step_ = t;
     cur_phase_ = "pivot search";
     void* Lt = elem(At_[v % 3], j * m * rows);
     if (j > 0) {
-      // column t after panel v-1 (look-ahead) and steps t0..t-1 of this panel
+      // column t after panel v-1 (look-ahead) and steps t0..t-1 of this panel; the pivot rows of
+      // those steps enter as 0 without a mask: their later panel columns were moved out (take_rows)
       dev_.wait(S_SIDE, ev_pp_[par][j - 1]);
       const int pe = prof_begin(S_SIDE);
       if (rows > 0) {
         // the update writes the new multipliers -X[:, t]^T (segment j of At) as it stores X[:, t]:
         // one launch fewer per step (emulated p = 4, N = 16384, direct 50 GB/s: 0.0533 / 0.0538 ->
         // 0.0518 / 0.0518 s; neutral elsewhere, profiles/side_chain_r3.md)
-        GemmExtra ex = pivot_rows_extra(par, j);
+        GemmExtra ex;
         ex.latency = true;
         ex.tneg = Lt;
         ex.ldtneg = rows;
@@ -677,34 +680,22 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
       prof_end(PH_COLUMN, pe, S_SIDE);
       select(t, Lt);
     }
-    wait_pivot((int)(t & 1), t, host_wait);
-    PivotResult r = piv_host_[t & 1];
-    if (!r.found && opt_.pivot == PivotRule::Partial) {
-      // every rank's largest-magnitude candidate was singular: this step takes the full search
-      st.pivot_fallbacks++;
-      select(t, Lt, /*full=*/true);
-      wait_pivot((int)(t & 1), t, host_wait);
-      r = piv_host_[t & 1];
+    bool owner = true;
+    int root = 0;
+    if (!ahead) {
+      PivotResult r;
+      if (!await_step(v, j, st, host_wait, r)) return false;
+      owner = (r.owner == L_.k);
+      root = r.owner;
     }
-    if (!r.found) {
-      comm_.drain_all(dev_);
-      st.status = Status::Singular;
-      st.singular_step = t;
-      return false;
-    }
-    piv_[par][j] = r;
-    st.pivots[t] = r.phys;
-    if (r.owner == L_.k) --live_;  // this rank's block row s_t is no longer a candidate
     cur_phase_ = "panel piece";
-    const bool owner = (r.owner == L_.k);
-    const int64_t sl = r.phys / L_.p;
     int pe = prof_begin(S_SIDE);
     if (owner) {
       st.bcast_bytes += double(m) * npad * es;
       // one launch: multipliers of row s_t for steps t0..t-1 -> Lrow (K-major j*m x m), H_t^T -> Ht,
       // and the multiplier rows of s_t become [0 .. 0 | I] (earlier segments 0, own segment I)
-      dev_.owner_edits(opt_.dtype, At_[v % 3], rows, sl * m, j, m, Lrow_[par][j], Ht_[par][j],
-                       elem(inv_, sl * m * m), S_SIDE);
+      dev_.owner_edits(opt_.dtype, At_[v % 3], rows, seq_ + t, L_.p, L_.k, j, m, Lrow_[par][j], Ht_[par][j], inv_,
+                       S_SIDE);
     }
     prof_end(PH_EDITS, pe, S_SIDE);
     dev_.record(ev_edit_[par], S_SIDE);
@@ -734,8 +725,10 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
       }
       if (j + 1 < q) {
         const int64_t w = (q - j - 1) * m;
-        dev_.copy2d(elem(RP_, (j + 1) * m), dm * es, elem(X_, sl * m * npad + (t0 + j + 1) * m),
-                    npad * es, w * es, m, S_SIDE);
+        // moved, not copied: these columns of the pivot row must enter the panel's next column
+        // updates as 0 (the sweep's pivot-row rule)
+        dev_.take_rows(opt_.dtype, elem(RP_, (j + 1) * m), dm, X_, npad, seq_ + t, L_.p, L_.k, (t0 + j + 1) * m, w,
+                       m, S_SIDE);
         if (j > 0) {
           GemmDesc& g = pr[np++];
           g.op = GemmOp::Acc;
@@ -750,11 +743,45 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
                 dm, S_SIDE, lat);
       dev_.h_block(opt_.dtype, elem(pp, j * m), dm, Ht_[par][j], m, S_SIDE);
     }
-    comm_.bcast_many(dev_, {BcastOp{pp, (size_t)m * dm * es, r.owner}}, S_SIDE);
+    comm_.bcast_many(dev_, {BcastOp{pp, (size_t)m * dm * es, root}}, S_SIDE);
     prof_end(PH_PIECES, pe, S_SIDE);
     dev_.record(ev_pp_[par][j], S_SIDE);
     dbg_sync();
   }
+  if (ahead) {  // the panel's pivots, in step order (the first singular step ends the solve)
+    cur_phase_ = "pivot search";
+    for (int64_t j = 0; j < q; ++j) {
+      PivotResult r;
+      if (!await_step(v, j, st, host_wait, r)) return false;
+    }
+  }
+  return true;
+}
+
+// The host side of step t0(v) + j: wait for its pivot (pinned slot), the --pivot partial fallback,
+// singular detection, book-keeping.  False when the matrix is singular at this step.
+bool Engine::await_step(int64_t v, int64_t j, SolveStats& st, double& host_wait, PivotResult& r) {
+  const int par = (int)(v & 1);
+  const int64_t t = panel_t0(v) + j;
+  cur_step_ = t;
+  wait_pivot(hslot(t), t, host_wait);
+  r = piv_host_[hslot(t)];
+  if (!r.found && opt_.pivot == PivotRule::Partial) {
+    // every rank's largest-magnitude candidate was singular: this step takes the full search
+    st.pivot_fallbacks++;
+    select(t, elem(At_[v % 3], j * L_.m * L_.rows), /*full=*/true);
+    wait_pivot(hslot(t), t, host_wait);
+    r = piv_host_[hslot(t)];
+  }
+  if (!r.found) {
+    comm_.drain_all(dev_);
+    st.status = Status::Singular;
+    st.singular_step = t;
+    return false;
+  }
+  piv_[par][j] = r;
+  st.pivots[t] = r.phys;
+  if (r.owner == L_.k) --live_;  // this rank's block row s_t is no longer a candidate
   return true;
 }
 
