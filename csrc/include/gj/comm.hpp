@@ -43,6 +43,11 @@ class Comm {
   virtual void bcast(Device& dev, void* buf, size_t bytes, int root, int s) = 0;
   virtual void allreduce_max(Device& dev, double* buf, size_t count, int s) = 0;
   virtual void group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) = 0;
+  // In-place sum of `count` elements of dtype dt over the ranks (every rank gets the same bits).
+  // Default: all-gather into a scratch buffer the communicator keeps (free_scratch) + an ordered
+  // device sum; RCCL uses ncclAllReduce.
+  virtual void allreduce_sum(Device& dev, void* buf, size_t count, DType dt, int s);
+  void free_scratch(Device& dev);
   // Several broadcasts (any roots) issued as one group: RCCL runs them concurrently, so pivot rows
   // owned by different ranks travel over different xGMI links at the same time.
   // Ops of at least direct_bcast_min() bytes take the two-round direct algorithm (bcast_direct).
@@ -112,6 +117,8 @@ class Comm {
   void bcast_direct(Device& dev, const std::vector<BcastOp>& ops, int s);
   size_t direct_min_ = 0;
   std::string bcast_report_;
+  void* sum_scratch_[kNumStreams] = {};
+  size_t sum_cap_[kNumStreams] = {};
 };
 
 // A trivial single-rank communicator.
@@ -125,6 +132,7 @@ class SelfComm : public Comm {
   }
   void bcast(Device&, void*, size_t, int, int) override {}
   void allreduce_max(Device&, double*, size_t, int) override {}
+  void allreduce_sum(Device&, void*, size_t, DType, int) override {}
   void group_p2p(Device&, const std::vector<P2POp>& ops, int) override {
     GJ_REQUIRE(ops.empty(), "SelfComm: point-to-point with a peer requested");
   }

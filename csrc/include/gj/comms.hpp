@@ -31,6 +31,7 @@ class RcclComm : public Comm {
   void bcast(Device& dev, void* buf, size_t bytes, int root, int s) override;
   void bcast_many(Device& dev, const std::vector<BcastOp>& ops, int s) override;
   void allreduce_max(Device& dev, double* buf, size_t count, int s) override;
+  void allreduce_sum(Device& dev, void* buf, size_t count, DType dt, int s) override;
   void group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) override;
   void barrier(Device& dev) override;
   double host_max(Device& dev, double v) override;
@@ -188,6 +189,8 @@ class ShadowComm : public Comm {
   void allgather(Device& dev, const void* send, void* recv, size_t bytes, int s) override;
   void bcast(Device& dev, void* buf, size_t bytes, int root, int s) override;
   void allreduce_max(Device&, double*, size_t, int) override {}
+  // ring all-reduce cost (2 (p-1)/p of the bytes over one link); the synthetic peers add zeros
+  void allreduce_sum(Device& dev, void* buf, size_t count, DType dt, int s) override;
   void group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) override;
   void barrier(Device& dev) override { dev.sync_all(); }
   double host_max(Device&, double v) override { return v; }

@@ -228,6 +228,12 @@ class Device {
   // enter the next column updates as 0 (the sweep's zero-row rule) without a zero-row mask.
   virtual void take_rows(DType dt, void* dst, int64_t ldd, void* X, int64_t ldx, const int32_t* phys, int64_t p,
                          int64_t k, int64_t col0, int64_t w, int64_t m, int s) = 0;
+  // dst[i] = sum over q < nslices of src[q*count + i], in q order (identical on every rank).
+  virtual void sum_slices(DType dt, void* dst, const void* src, int64_t count, int64_t nslices, int s) = 0;
+  // buf[0 .. count) = 0 unless this rank owns the pivot g = *phys (g % p == k): the non-owners'
+  // share of a root-agnostic exchange (an all-reduce sum carries the owner's values).
+  virtual void zero_unless_owner(DType dt, void* buf, int64_t count, const int32_t* phys, int64_t p, int64_t k,
+                                 int s) = 0;
   virtual void h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, int s) = 0;
   virtual void gemm(DType dt, GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const void* A,
                     int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int s,

@@ -178,10 +178,15 @@ class Engine {
   // enqueues a whole panel's steps before it reads any result)
   static constexpr int kPivSlots = 2 * kMaxDepth;
   static int hslot(int64_t t) { return (int)(t % kPivSlots); }
-  // One rank and the reference pivot rule: the pivot chain is enqueued a panel at a time, every
-  // owner-side launch reading the pivot from device memory, the host reading the results after it
-  // (no host round trip per step).  Elsewhere the host needs each root before it can broadcast.
-  bool host_free_chain() const { return L_.p == 1 && opt_.pivot == PivotRule::MinInvNorm && !opt_.sync_debug; }
+  // The reference pivot rule: the pivot chain is enqueued a panel at a time, every owner-side
+  // launch reading the pivot from device memory, the host reading the results after it (no host
+  // round trip per step).  One rank always; p > 1 with host_free_multi_ (GJ_HOST_FREE), where the
+  // panel piece travels by a root-agnostic all-reduce (non-owners contribute zeros) because a
+  // broadcast needs its root on the host.
+  bool host_free_chain() const {
+    return opt_.pivot == PivotRule::MinInvNorm && !opt_.sync_debug && (L_.p == 1 || host_free_multi_);
+  }
+  bool host_free_multi_ = false;
   // 0 = ok, 1 = the work space does not fit, 2 = the matrix panels do not fit (why: the reason)
   int alloc_buffers(std::string& why);
   void alloc_work(int64_t wmax);

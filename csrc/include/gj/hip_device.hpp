@@ -81,6 +81,9 @@ class HipDevice : public Device {
                    int64_t m, void* lrow, void* ht, const void* inv, int s) override;
   void take_rows(DType dt, void* dst, int64_t ldd, void* X, int64_t ldx, const int32_t* phys, int64_t p, int64_t k,
                  int64_t col0, int64_t w, int64_t m, int s) override;
+  void sum_slices(DType dt, void* dst, const void* src, int64_t count, int64_t nslices, int s) override;
+  void zero_unless_owner(DType dt, void* buf, int64_t count, const int32_t* phys, int64_t p, int64_t k,
+                         int s) override;
   void h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, int s) override;
   void gemm(DType dt, GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const void* A,
             int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int s,

@@ -87,6 +87,8 @@ void owner_edits(DType dt, void* At, int64_t ldl, const int32_t* phys, int64_t p
                  int64_t m, void* lrow, void* ht, const void* inv, hipStream_t s);
 void take_rows(DType dt, void* dst, int64_t ldd, void* X, int64_t ldx, const int32_t* phys, int64_t p, int64_t k,
                int64_t col0, int64_t w, int64_t m, hipStream_t s);
+void sum_slices(DType dt, void* dst, const void* src, int64_t count, int64_t nslices, hipStream_t s);
+void zero_unless_owner(DType dt, void* buf, int64_t count, const int32_t* phys, int64_t p, int64_t k, hipStream_t s);
 void h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, hipStream_t s);
 void permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx, int64_t nblk,
                     int64_t m, int64_t Nr, const int32_t* dst_blk, const int32_t* colsrc,

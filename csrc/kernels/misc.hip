@@ -413,6 +413,48 @@ void take_rows(DType dt, void* dst, int64_t ldd, void* X, int64_t ldx, const int
                        static_cast<float*>(X), ldx, phys, p, k, col0, w, m);
 }
 
+// ---------------------------------------------------------------- root-agnostic exchange helpers
+template <typename T>
+__global__ __launch_bounds__(256) void sum_slices_kernel(T* __restrict__ dst, const T* __restrict__ src, int64_t count,
+                                                         int64_t nslices) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
+    T acc = src[i];
+    for (int64_t q = 1; q < nslices; ++q) acc += src[q * count + i];
+    dst[i] = acc;
+  }
+}
+
+void sum_slices(DType dt, void* dst, const void* src, int64_t count, int64_t nslices, hipStream_t s) {
+  if (count <= 0) return;
+  const unsigned grid = grid_for(count, 256, 1024);
+  if (dt == DType::F64)
+    hipLaunchKernelGGL(sum_slices_kernel<double>, dim3(grid), dim3(256), 0, s, static_cast<double*>(dst),
+                       static_cast<const double*>(src), count, nslices);
+  else
+    hipLaunchKernelGGL(sum_slices_kernel<float>, dim3(grid), dim3(256), 0, s, static_cast<float*>(dst),
+                       static_cast<const float*>(src), count, nslices);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void zero_unless_owner_kernel(T* buf, int64_t count, const int32_t* __restrict__ phys,
+                                                                int64_t p, int64_t k) {
+  const int64_t g = *phys;
+  if (g >= 0 && g % p == k) return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x)
+    buf[i] = T(0);
+}
+
+void zero_unless_owner(DType dt, void* buf, int64_t count, const int32_t* phys, int64_t p, int64_t k, hipStream_t s) {
+  if (count <= 0) return;
+  const unsigned grid = grid_for(count, 256, 1024);
+  if (dt == DType::F64)
+    hipLaunchKernelGGL(zero_unless_owner_kernel<double>, dim3(grid), dim3(256), 0, s, static_cast<double*>(buf), count,
+                       phys, p, k);
+  else
+    hipLaunchKernelGGL(zero_unless_owner_kernel<float>, dim3(grid), dim3(256), 0, s, static_cast<float*>(buf), count,
+                       phys, p, k);
+}
+
 // ---------------------------------------------------------------- permute_blocks
 template <typename T>
 __global__ __launch_bounds__(256) void permute_kernel(T* __restrict__ dst, int64_t ldd,

@@ -296,6 +296,13 @@ void AsyncHostDevice::take_rows(DType dt, void* dst, int64_t ldd, void* X, int64
                                 int64_t p, int64_t k, int64_t col0, int64_t w, int64_t m, int s) {
   enqueue(s, [=] { inner_.take_rows(dt, dst, ldd, X, ldx, phys, p, k, col0, w, m, s); });
 }
+void AsyncHostDevice::sum_slices(DType dt, void* dst, const void* src, int64_t count, int64_t nslices, int s) {
+  enqueue(s, [=] { inner_.sum_slices(dt, dst, src, count, nslices, s); });
+}
+void AsyncHostDevice::zero_unless_owner(DType dt, void* buf, int64_t count, const int32_t* phys, int64_t p, int64_t k,
+                                        int s) {
+  enqueue(s, [=] { inner_.zero_unless_owner(dt, buf, count, phys, p, k, s); });
+}
 void AsyncHostDevice::h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, int s) {
   enqueue(s, [=] { inner_.h_block(dt, R, ldr, Ht, m, s); });
 }

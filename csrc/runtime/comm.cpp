@@ -217,4 +217,32 @@ std::string Comm::tune_bcast(Device& dev, std::vector<size_t> sizes) {
   return thr == 0 ? "ring" : "direct";
 }
 
+// Generic sum: every rank's contribution gathered (stream-ordered, the transport's all-gather), then
+// summed in rank order on the device, so every rank computes the same bits.  The scratch is kept
+// per stream role (the engine frees it, free_scratch) -- freeing per call would synchronise.
+void Comm::allreduce_sum(Device& dev, void* buf, size_t count, DType dt, int s) {
+  if (size() == 1 || count == 0) return;
+  const size_t bytes = count * dtype_size(dt), need = bytes * (size_t)size();
+  if (sum_cap_[s] < need) {
+    if (sum_scratch_[s]) {
+      dev.sync_all();
+      dev.release(sum_scratch_[s]);
+    }
+    sum_scratch_[s] = dev.alloc(need);
+    sum_cap_[s] = need;
+    dev.label(sum_scratch_[s], "comm sum scratch");
+  }
+  allgather(dev, buf, sum_scratch_[s], bytes, s);
+  dev.sum_slices(dt, buf, sum_scratch_[s], (int64_t)count, size(), s);
+}
+
+void Comm::free_scratch(Device& dev) {
+  for (int s = 0; s < kNumStreams; ++s)
+    if (sum_scratch_[s]) {
+      dev.release(sum_scratch_[s]);
+      sum_scratch_[s] = nullptr;
+      sum_cap_[s] = 0;
+    }
+}
+
 }  // namespace gj

@@ -302,6 +302,15 @@ void HipDevice::take_rows(DType dt, void* dst, int64_t ldd, void* X, int64_t ldx
   kern::take_rows(dt, dst, ldd, X, ldx, phys, p, k, col0, w, m, hs(streams_[s]));
   check_launch();
 }
+void HipDevice::sum_slices(DType dt, void* dst, const void* src, int64_t count, int64_t nslices, int s) {
+  kern::sum_slices(dt, dst, src, count, nslices, hs(streams_[s]));
+  check_launch();
+}
+void HipDevice::zero_unless_owner(DType dt, void* buf, int64_t count, const int32_t* phys, int64_t p, int64_t k,
+                                  int s) {
+  kern::zero_unless_owner(dt, buf, count, phys, p, k, hs(streams_[s]));
+  check_launch();
+}
 void HipDevice::h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, int s) {
   kern::h_block(dt, R, ldr, Ht, m, hs(streams_[s]));
   check_launch();

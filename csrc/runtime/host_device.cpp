@@ -381,6 +381,26 @@ void HostDevice::take_rows(DType dt, void* dst, int64_t ldd, void* X, int64_t ld
   }
 }
 
+void HostDevice::sum_slices(DType dt, void* dst, const void* src, int64_t count, int64_t nslices, int) {
+  auto run = [&](auto* d, const auto* x) {
+    using T = std::remove_pointer_t<decltype(d)>;
+    for (int64_t i = 0; i < count; ++i) {
+      T acc = x[i];
+      for (int64_t q = 1; q < nslices; ++q) acc += x[q * count + i];
+      d[i] = acc;
+    }
+  };
+  if (dt == DType::F64) run(static_cast<double*>(dst), static_cast<const double*>(src));
+  else run(static_cast<float*>(dst), static_cast<const float*>(src));
+}
+
+void HostDevice::zero_unless_owner(DType dt, void* buf, int64_t count, const int32_t* phys, int64_t p, int64_t k,
+                                   int) {
+  const int64_t g = *phys;
+  if (g >= 0 && g % p == k) return;
+  std::memset(buf, 0, (size_t)count * dtype_size(dt));
+}
+
 void HostDevice::h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, int) {
   for (int64_t i = 0; i < m; ++i)
     for (int64_t j = 0; j < m; ++j) {

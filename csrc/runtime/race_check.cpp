@@ -637,6 +637,16 @@ void RaceCheckDevice::take_rows(DType dt, void* dst, int64_t ldd, void* X, int64
   check(s, "take_rows", {R(span(phys, 4), "phys"), W(xr, "X piece"), W(rect(dst, ldd, w, m, es), "dst")});
   inner_->take_rows(dt, dst, ldd, X, ldx, phys, p, k, col0, w, m, s);
 }
+void RaceCheckDevice::sum_slices(DType dt, void* dst, const void* src, int64_t count, int64_t nslices, int s) {
+  const int64_t es = (int64_t)dtype_size(dt);
+  check(s, "sum_slices", {R(span(src, count * nslices * es), "slices"), W(span(dst, count * es), "dst")});
+  inner_->sum_slices(dt, dst, src, count, nslices, s);
+}
+void RaceCheckDevice::zero_unless_owner(DType dt, void* buf, int64_t count, const int32_t* phys, int64_t p,
+                                        int64_t k, int s) {
+  check(s, "zero_unless_owner", {R(span(phys, 4), "phys"), W(span(buf, count * (int64_t)dtype_size(dt)), "buf")});
+  inner_->zero_unless_owner(dt, buf, count, phys, p, k, s);
+}
 void RaceCheckDevice::h_block(DType dt, void* Rp, int64_t ldr, const void* Ht, int64_t m, int s) {
   const int64_t es = (int64_t)dtype_size(dt);
   check(s, "h_block", {R(span(Ht, m * m * es), "Ht"), W(rect(Rp, ldr, m, m, es), "R")});

@@ -117,6 +117,13 @@ void RcclComm::allreduce_max(Device& dev, double* buf, size_t count, int s) {
   NCCL_OK(ncclAllReduce(buf, buf, count, ncclFloat64, ncclMax, static_cast<ncclComm_t>(comm_for(s)), st(dev, s)));
 }
 
+void RcclComm::allreduce_sum(Device& dev, void* buf, size_t count, DType dt, int s) {
+  if (n_ == 1 || count == 0) return;
+  note(s, "ncclAllReduce(sum)", count * dtype_size(dt));
+  NCCL_OK(ncclAllReduce(buf, buf, count, dt == DType::F64 ? ncclFloat64 : ncclFloat32, ncclSum,
+                        static_cast<ncclComm_t>(comm_for(s)), st(dev, s)));
+}
+
 void RcclComm::group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) {
   if (ops.empty()) return;
   ncclComm_t c = static_cast<ncclComm_t>(comm_for(s));

@@ -85,6 +85,10 @@ void ShadowComm::allgather(Device& dev, const void* send, void* recv, size_t byt
   dev.copy(static_cast<char*>(recv) + bytes, reinterpret_cast<char*>(recs) + bytes, (p_ - 1) * bytes, s);
 }
 
+void ShadowComm::allreduce_sum(Device& dev, void*, size_t count, DType dt, int s) {
+  cost(dev, 2 * count * dtype_size(dt) * (size_t)(p_ - 1) / (size_t)p_, 1, s);
+}
+
 void ShadowComm::bcast(Device& dev, void* buf, size_t bytes, int root, int s) {
   if (use_direct(bytes)) return bcast_direct(dev, {BcastOp{buf, bytes, root}}, s);
   cost(dev, bytes, 1, s);

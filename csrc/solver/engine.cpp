@@ -188,12 +188,14 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // but N = 16384 +1.1 % and N = 32768 +0.7 % (more COMM workgroups beside the trailing update), so
   // only where the pivot chain dominates (padded order <= 8192).  GJ_COMM_SMALL_TILES overrides.
   comm_small_tiles_ = L_.npad <= 8192;
+  if (const char* e = std::getenv("GJ_HOST_FREE")) host_free_multi_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("GJ_COMM_SMALL_TILES")) comm_small_tiles_ = std::atoi(e) != 0;
 
 }
 
 Engine::~Engine() {
   free_buffers();
+  comm_.free_scratch(dev_);
   dev_.trace_context(nullptr, nullptr);
 }
 
@@ -691,7 +693,6 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
     cur_phase_ = "panel piece";
     int pe = prof_begin(S_SIDE);
     if (owner) {
-      st.bcast_bytes += double(m) * npad * es;
       // one launch: multipliers of row s_t for steps t0..t-1 -> Lrow (K-major j*m x m), H_t^T -> Ht,
       // and the multiplier rows of s_t become [0 .. 0 | I] (earlier segments 0, own segment I)
       dev_.owner_edits(opt_.dtype, At_[v % 3], rows, seq_ + t, L_.p, L_.k, j, m, Lrow_[par][j], Ht_[par][j], inv_,
@@ -743,7 +744,13 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
                 dm, S_SIDE, lat);
       dev_.h_block(opt_.dtype, elem(pp, j * m), dm, Ht_[par][j], m, S_SIDE);
     }
-    comm_.bcast_many(dev_, {BcastOp{pp, (size_t)m * dm * es, root}}, S_SIDE);
+    if (ahead && L_.p > 1) {
+      // root-agnostic: every rank computed a piece, only the owner's survives the sum
+      dev_.zero_unless_owner(opt_.dtype, pp, m * dm, seq_ + t, L_.p, L_.k, S_SIDE);
+      comm_.allreduce_sum(dev_, pp, (size_t)m * dm, opt_.dtype, S_SIDE);
+    } else {
+      comm_.bcast_many(dev_, {BcastOp{pp, (size_t)m * dm * es, root}}, S_SIDE);
+    }
     prof_end(PH_PIECES, pe, S_SIDE);
     dev_.record(ev_pp_[par][j], S_SIDE);
     dbg_sync();
@@ -781,7 +788,10 @@ bool Engine::await_step(int64_t v, int64_t j, SolveStats& st, double& host_wait,
   }
   piv_[par][j] = r;
   st.pivots[t] = r.phys;
-  if (r.owner == L_.k) --live_;  // this rank's block row s_t is no longer a candidate
+  if (r.owner == L_.k) {
+    --live_;  // this rank's block row s_t is no longer a candidate
+    st.bcast_bytes += double(L_.m) * L_.npad * esz();
+  }
   return true;
 }
 

@@ -132,3 +132,19 @@ def test_cli_race_check(gj_bin):
                         "random", "200", "20"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 2
     assert "race: unordered" in r.stderr
+
+
+@pytest.mark.parametrize("p", [2, 3, 8])
+@pytest.mark.parametrize("depth", [1, 2, 4])
+def test_host_free_chain_multi_rank(p, depth, monkeypatch):
+    """GJ_HOST_FREE=1 at p > 1: a panel's pivot chain is enqueued without a host wait per step, the
+    owner-side launches read the pivot on the device and the panel piece travels by an all-reduce
+    sum (non-owners contribute zeros).  Race-free, and bit-identical to the host-driven schedule."""
+    ref = gj.GaussJordan(block_size=20, ranks=p, device="cpu", comm="async", depth=depth,
+                         host_threads=1).run(420, gen="random", seed=3, keep_inverse=True)
+    monkeypatch.setenv("GJ_HOST_FREE", "1")
+    rep = _run(420, 20, p, depth=depth, jitter_us=20.0)
+    assert rep["race_count"] == 0, "\n".join(rep["races"])
+    got = gj.GaussJordan(block_size=20, ranks=p, device="cpu", comm="async", depth=depth,
+                         host_threads=1).run(420, gen="random", seed=3, keep_inverse=True)
+    assert np.array_equal(got["inverse"], ref["inverse"])
