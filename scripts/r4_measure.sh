@@ -20,3 +20,8 @@ for hf in 0 1; do
   GJ_HOST_FREE=$hf timeout -k 10 300 python bench/bench_emulate.py --ranks 8 --size 32768 --reps 1 --bw 50 --bcast direct > $o/emu32k_hf$hf.txt 2>&1 || exit $?
   cat $o/emu32k_hf$hf.txt | tail -2
 done
+# the 32-CU reservation of the p = 8 ranks, re-checked now that no dead inverse workgroup is dispatched
+for rc in 0 32; do
+  GJ_RESERVE_CUS=$rc timeout -k 10 300 python bench/bench_emulate.py --ranks 8 --size 32768 --reps 1 --bw 50 --bcast direct > $o/emu32k_res$rc.txt 2>&1 || exit $?
+  cat $o/emu32k_res$rc.txt | tail -2
+done
