@@ -54,6 +54,22 @@ struct GemmExtra {
   int64_t tneg_cols = 0;
 };
 
+// Owner-side piece work fused into Device::owner_edits (all optional; w = 0 / eye = null: none):
+// the pivot row's later panel columns moved out of X, dst[r*ldd + c] = X[(row0+r)*ldx + col0 + c],
+// then zeroed in X (r < m, c < w; the next column updates need them as 0), and the m x m identity
+// written at eye (ld ld_eye) -- the pivot's own block of the piece GEMM's B, so H_t lands in the
+// piece without a separate copy (H I = H exactly).
+struct PieceMove {
+  void* dst = nullptr;
+  int64_t ldd = 0;
+  void* X = nullptr;
+  int64_t ldx = 0;
+  int64_t col0 = 0;
+  int64_t w = 0;
+  void* eye = nullptr;
+  int64_t ld_eye = 0;
+};
+
 // One product of a batched small-GEMM launch (Device::gemm_batch): C (+)= A B, A K-major.
 struct GemmDesc {
   GemmOp op = GemmOp::Acc;
@@ -220,8 +236,10 @@ class Device {
   // lrow[kk*m + c] = At[kk*ldl + row0 + c] for kk < j*m, set those rows of At to [0 .. 0 | I] over
   // the first (j+1)*m K-rows (identity in segment j), and copy the block's inverse:
   // ht[e] = inv[b*m*m + e], e < m*m.
+  // mv: the PieceMove work of the same pivot, in the same launch.
   virtual void owner_edits(DType dt, void* At, int64_t ldl, const int32_t* phys, int64_t p, int64_t k,
-                           int64_t j, int64_t m, void* lrow, void* ht, const void* inv, int s) = 0;
+                           int64_t j, int64_t m, void* lrow, void* ht, const void* inv, const PieceMove& mv,
+                           int s) = 0;
   // Take the pivot row's piece (device-addressed like owner_edits): for g = *phys owned here (else
   // nothing), local rows row0 = (g / p) m .. + m:  dst[r*ldd + c] = X[(row0 + r)*ldx + col0 + c],
   // then X[row0 + r][col0 + c] = 0, for r < m, c < w.  The panel's later columns of a pivot row

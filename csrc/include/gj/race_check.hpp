@@ -219,7 +219,7 @@ class RaceCheckDevice : public Device {
                            int32_t* phys_at, int32_t* used, int32_t* seq, PivotRec* rec, PivotResult* out,
                            PivotResult* host_out, int s) override;
   void owner_edits(DType dt, void* At, int64_t ldl, const int32_t* phys, int64_t p, int64_t k, int64_t j,
-                   int64_t m, void* lrow, void* ht, const void* inv, int s) override;
+                   int64_t m, void* lrow, void* ht, const void* inv, const PieceMove& mv, int s) override;
   void take_rows(DType dt, void* dst, int64_t ldd, void* X, int64_t ldx, const int32_t* phys, int64_t p, int64_t k,
                  int64_t col0, int64_t w, int64_t m, int s) override;
   void sum_slices(DType dt, void* dst, const void* src, int64_t count, int64_t nslices, int s) override;

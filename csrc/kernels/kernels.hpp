@@ -84,7 +84,7 @@ void pivot_select_single(const double* scores, const int32_t* valid, const Layou
 void pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos, int32_t* phys_at,
                   int32_t* used, int32_t* seq, PivotResult* out, PivotResult* host_out, hipStream_t s);
 void owner_edits(DType dt, void* At, int64_t ldl, const int32_t* phys, int64_t p, int64_t k, int64_t j,
-                 int64_t m, void* lrow, void* ht, const void* inv, hipStream_t s);
+                 int64_t m, void* lrow, void* ht, const void* inv, const PieceMove& mv, hipStream_t s);
 void take_rows(DType dt, void* dst, int64_t ldd, void* X, int64_t ldx, const int32_t* phys, int64_t p, int64_t k,
                int64_t col0, int64_t w, int64_t m, hipStream_t s);
 void sum_slices(DType dt, void* dst, const void* src, int64_t count, int64_t nslices, hipStream_t s);

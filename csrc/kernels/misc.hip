@@ -350,39 +350,50 @@ void commit_candidate(DType dt, void* inv_t, const void* inv1, const int32_t* va
 // ---------------------------------------------------------------- owner edits (one launch)
 // The pivot comes from device memory (the step's pivot-sequence entry): the launch can be enqueued
 // before the host has seen the pivot, and is a no-op on ranks that do not own it.
+// Work items in one flat range: the At row edits, the H copy, then (PieceMove) the pivot row's
+// piece moved out of X and the identity block.
 template <typename T>
 __global__ __launch_bounds__(256) void owner_edits_kernel(T* At, int64_t ldl, const int32_t* __restrict__ phys,
                                                           int64_t p, int64_t k, int64_t j, int64_t m, T* lrow, T* ht,
-                                                          const T* inv) {
+                                                          const T* inv, PieceMove mv) {
   const int64_t g = *phys;
   if (g < 0 || g % p != k) return;
   const int64_t b = g / p, row0 = b * m;
   const T* inv_blk = inv + b * m * m;
   const int64_t nrow = (j + 1) * m, total = nrow * m;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total + m * m;
-       e += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t e1 = total + m * m, e2 = e1 + m * mv.w, e3 = e2 + (mv.eye ? m * m : 0);
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < e3; e += (int64_t)gridDim.x * blockDim.x) {
     if (e < total) {
       const int64_t kk = e / m, c = e - kk * m;
       T* x = At + kk * ldl + row0 + c;
       if (kk < j * m) lrow[kk * m + c] = *x;
       *x = (kk - j * m == c) ? T(1) : T(0);
-    } else {
+    } else if (e < e1) {
       ht[e - total] = inv_blk[e - total];
+    } else if (e < e2) {
+      const int64_t r = (e - e1) / mv.w, c = (e - e1) - r * mv.w;
+      T* x = static_cast<T*>(mv.X) + (row0 + r) * mv.ldx + mv.col0 + c;
+      static_cast<T*>(mv.dst)[r * mv.ldd + c] = *x;
+      *x = T(0);
+    } else {
+      const int64_t r = (e - e2) / m, c = (e - e2) - r * m;
+      static_cast<T*>(mv.eye)[r * mv.ld_eye + c] = (r == c) ? T(1) : T(0);
     }
   }
 }
 
 void owner_edits(DType dt, void* At, int64_t ldl, const int32_t* phys, int64_t p, int64_t k, int64_t j,
-                 int64_t m, void* lrow, void* ht, const void* inv, hipStream_t s) {
-  const int64_t work = (j + 2) * m * m;
+                 int64_t m, void* lrow, void* ht, const void* inv, const PieceMove& mv, hipStream_t s) {
+  const int64_t work = (j + 2) * m * m + m * mv.w + (mv.eye ? m * m : 0);
   const unsigned grid = grid_for(work, 256, 256);
   if (dt == DType::F64)
     hipLaunchKernelGGL(owner_edits_kernel<double>, dim3(grid), dim3(256), 0, s, static_cast<double*>(At), ldl, phys,
                        p, k, j, m, static_cast<double*>(lrow), static_cast<double*>(ht),
-                       static_cast<const double*>(inv));
+                       static_cast<const double*>(inv), mv);
   else
     hipLaunchKernelGGL(owner_edits_kernel<float>, dim3(grid), dim3(256), 0, s, static_cast<float*>(At), ldl, phys, p,
-                       k, j, m, static_cast<float*>(lrow), static_cast<float*>(ht), static_cast<const float*>(inv));
+                       k, j, m, static_cast<float*>(lrow), static_cast<float*>(ht), static_cast<const float*>(inv),
+                       mv);
 }
 
 // The pivot row's piece of the panel's later columns, moved out (copied, then zeroed in X).

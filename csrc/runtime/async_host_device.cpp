@@ -289,8 +289,9 @@ void AsyncHostDevice::pivot_global_now(const PivotRec* recs, int32_t p, int32_t 
   }
 }
 void AsyncHostDevice::owner_edits(DType dt, void* At, int64_t ldl, const int32_t* phys, int64_t p, int64_t k,
-                                  int64_t j, int64_t m, void* lrow, void* ht, const void* inv, int s) {
-  enqueue(s, [=] { inner_.owner_edits(dt, At, ldl, phys, p, k, j, m, lrow, ht, inv, s); });
+                                  int64_t j, int64_t m, void* lrow, void* ht, const void* inv, const PieceMove& mv,
+                                  int s) {
+  enqueue(s, [=] { inner_.owner_edits(dt, At, ldl, phys, p, k, j, m, lrow, ht, inv, mv, s); });
 }
 void AsyncHostDevice::take_rows(DType dt, void* dst, int64_t ldd, void* X, int64_t ldx, const int32_t* phys,
                                 int64_t p, int64_t k, int64_t col0, int64_t w, int64_t m, int s) {

@@ -293,8 +293,8 @@ void HipDevice::pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t
   check_launch();
 }
 void HipDevice::owner_edits(DType dt, void* At, int64_t ldl, const int32_t* phys, int64_t p, int64_t k, int64_t j,
-                            int64_t m, void* lrow, void* ht, const void* inv, int s) {
-  kern::owner_edits(dt, At, ldl, phys, p, k, j, m, lrow, ht, inv, hs(streams_[s]));
+                            int64_t m, void* lrow, void* ht, const void* inv, const PieceMove& mv, int s) {
+  kern::owner_edits(dt, At, ldl, phys, p, k, j, m, lrow, ht, inv, mv, hs(streams_[s]));
   check_launch();
 }
 void HipDevice::take_rows(DType dt, void* dst, int64_t ldd, void* X, int64_t ldx, const int32_t* phys, int64_t p,

@@ -348,9 +348,20 @@ void HostDevice::pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_
 }
 
 void HostDevice::owner_edits(DType dt, void* At, int64_t ldl, const int32_t* phys, int64_t p, int64_t k,
-                             int64_t j, int64_t m, void* lrow, void* ht, const void* inv, int) {
+                             int64_t j, int64_t m, void* lrow, void* ht, const void* inv, const PieceMove& mv,
+                             int s) {
   const int64_t g = *phys;
   if (g < 0 || g % p != k) return;
+  if (mv.w > 0) take_rows(dt, mv.dst, mv.ldd, mv.X, mv.ldx, phys, p, k, mv.col0, mv.w, m, s);
+  if (mv.eye) {
+    const size_t es = dtype_size(dt);
+    for (int64_t r = 0; r < m; ++r)
+      for (int64_t c = 0; c < m; ++c) {
+        char* e = static_cast<char*>(mv.eye) + (r * mv.ld_eye + c) * (int64_t)es;
+        if (dt == DType::F64) *reinterpret_cast<double*>(e) = r == c ? 1.0 : 0.0;
+        else *reinterpret_cast<float*>(e) = r == c ? 1.0f : 0.0f;
+      }
+  }
   const int64_t row0 = (g / p) * m;
   auto run = [&](auto* a, auto* lr, auto* h, const auto* iv) {
     using T = std::remove_pointer_t<decltype(a)>;

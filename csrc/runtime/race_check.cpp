@@ -618,15 +618,24 @@ void RaceCheckDevice::pivot_select_single(const double* scores, const int32_t* v
   if (host_out) hb_->release_point(host_out, id_, s);
 }
 void RaceCheckDevice::owner_edits(DType dt, void* At, int64_t ldl, const int32_t* phys, int64_t p, int64_t k,
-                                  int64_t j, int64_t m, void* lrow, void* ht, const void* inv, int s) {
+                                  int64_t j, int64_t m, void* lrow, void* ht, const void* inv, const PieceMove& mv,
+                                  int s) {
   const int64_t es = (int64_t)dtype_size(dt);
   // the pivot's rows are chosen on the device: every row of the first (j + 1) m K-rows, every block
-  // of the inverses (height / width -1: to the end of the allocation)
+  // of the inverses, the piece's column range of every row of X (height / width -1: to the end of
+  // the allocation)
   std::vector<Acc> a{R(span(phys, 4), "phys"), W(rect(At, ldl, ldl, (j + 1) * m, es), "At rows"),
                      W(span(ht, m * m * es), "Ht"), R(MemRegion{static_cast<const char*>(inv), -1, -1, 1}, "inv")};
   if (j > 0) a.push_back(W(span(lrow, j * m * m * es), "Lrow"));
+  if (mv.w > 0) {
+    MemRegion xr = rect(static_cast<char*>(mv.X) + mv.col0 * es, mv.ldx, mv.w, 2, es);
+    xr.height = -1;
+    a.push_back(W(xr, "X piece"));
+    a.push_back(W(rect(mv.dst, mv.ldd, mv.w, m, es), "piece"));
+  }
+  if (mv.eye) a.push_back(W(rect(mv.eye, mv.ld_eye, m, m, es), "eye"));
   check(s, "owner_edits", a);
-  inner_->owner_edits(dt, At, ldl, phys, p, k, j, m, lrow, ht, inv, s);
+  inner_->owner_edits(dt, At, ldl, phys, p, k, j, m, lrow, ht, inv, mv, s);
 }
 void RaceCheckDevice::take_rows(DType dt, void* dst, int64_t ldd, void* X, int64_t ldx, const int32_t* phys,
                                 int64_t p, int64_t k, int64_t col0, int64_t w, int64_t m, int s) {

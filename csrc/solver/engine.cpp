@@ -695,8 +695,22 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
     if (owner) {
       // one launch: multipliers of row s_t for steps t0..t-1 -> Lrow (K-major j*m x m), H_t^T -> Ht,
       // and the multiplier rows of s_t become [0 .. 0 | I] (earlier segments 0, own segment I)
+      // ... and, same launch, the pivot row's later panel columns moved into RP (they must enter the
+      // panel's next column updates as 0: the sweep's pivot-row rule) and the identity block of RP
+      // at the pivot's own columns (the piece GEMM then writes H_t there)
+      PieceMove mv;
+      if (j + 1 < q) {
+        mv.dst = elem(RP_, (j + 1) * m);
+        mv.ldd = dm;
+        mv.X = X_;
+        mv.ldx = npad;
+        mv.col0 = (t0 + j + 1) * m;
+        mv.w = (q - j - 1) * m;
+      }
+      mv.eye = elem(RP_, j * m);
+      mv.ld_eye = dm;
       dev_.owner_edits(opt_.dtype, At_[v % 3], rows, seq_ + t, L_.p, L_.k, j, m, Lrow_[par][j], Ht_[par][j], inv_,
-                       S_SIDE);
+                       mv, S_SIDE);
     }
     prof_end(PH_EDITS, pe, S_SIDE);
     dev_.record(ev_edit_[par], S_SIDE);
@@ -725,11 +739,7 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
         g.C = elem(RP_, jc * m); g.ldc = dm;
       }
       if (j + 1 < q) {
-        const int64_t w = (q - j - 1) * m;
-        // moved, not copied: these columns of the pivot row must enter the panel's next column
-        // updates as 0 (the sweep's pivot-row rule)
-        dev_.take_rows(opt_.dtype, elem(RP_, (j + 1) * m), dm, X_, npad, seq_ + t, L_.p, L_.k, (t0 + j + 1) * m, w,
-                       m, S_SIDE);
+        const int64_t w = (q - j - 1) * m;  // moved out of X by owner_edits above
         if (j > 0) {
           GemmDesc& g = pr[np++];
           g.op = GemmOp::Acc;
@@ -742,7 +752,6 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
       dev_.gemm_batch(opt_.dtype, pr, np, S_SIDE);
       dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, q * m, m, Ht_[par][j], m, RP_, dm, pp,
                 dm, S_SIDE, lat);
-      dev_.h_block(opt_.dtype, elem(pp, j * m), dm, Ht_[par][j], m, S_SIDE);
     }
     if (ahead && L_.p > 1) {
       // root-agnostic: every rank computed a piece, only the owner's survives the sum
