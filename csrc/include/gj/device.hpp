@@ -52,6 +52,10 @@ struct GemmExtra {
   void* tneg = nullptr;
   int64_t ldtneg = 0;
   int64_t tneg_cols = 0;
+  // Owner-predicated launch (the host-free pivot chain at p > 1): the GEMM does nothing unless this
+  // rank owns the pivot g = *owner_phys (g % owner_p == owner_k) -- read on the device.
+  const int32_t* owner_phys = nullptr;
+  int64_t owner_p = 1, owner_k = 0;
 };
 
 // Owner-side piece work fused into Device::owner_edits (all optional; w = 0 / eye = null: none):

@@ -142,7 +142,16 @@ struct GemmArgs {
   int group;        // LDS-DMA kernel: tile rows per column-walk group (1 = row-major tile order)
   void* tneg;       // GemmExtra::tneg: -C^T of the columns < tncols also written here
   int64_t ldt, tncols;
+  const int32_t* pred;  // GemmExtra::owner_phys: skip unless *pred % pred_p == pred_k
+  int64_t pred_p, pred_k;
 };
+
+// GemmExtra::owner_phys: the whole launch is a no-op on ranks that do not own the pivot
+__device__ __forceinline__ bool gemm_skipped(const GemmArgs& g) {
+  if (g.pred == nullptr) return false;
+  const int64_t gg = *g.pred;
+  return gg < 0 || gg % g.pred_p != g.pred_k;
+}
 
 // XCD-aware bijective remap: blocks b and b+8 share an XCD (MI355X_MICROARCH.md §Workgroup
 // dispatch); give every XCD a contiguous range of tiles so neighbouring tiles share L2 lines.
@@ -375,6 +384,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, const int tile) {
 
 template <typename T, int AL, int MODE, typename CF>
 __global__ __launch_bounds__(CF::NT, CF::WAVES_PER_SIMD) void gemm_kernel(GemmArgs g) {
+  if (gemm_skipped(g)) return;
   gemm_tile<T, AL, MODE, CF>(g, xcd_remap((int)blockIdx.x, g.tiles_m * g.tiles_n));
 }
 
@@ -391,6 +401,7 @@ struct GemmBatch {
 
 template <typename T, typename CF>
 __global__ __launch_bounds__(CF::NT, CF::WAVES_PER_SIMD) void gemm_batch_kernel(GemmBatch b) {
+  if (gemm_skipped(b.a[0])) return;  // one predicate per batch (fill: every product's, identical)
   const int bid = (int)blockIdx.x;
   int i = 0;
 #pragma unroll
@@ -454,6 +465,7 @@ __device__ __forceinline__ void wait_pieces(int n) {
 template <int MODE, int NS, int OCC, int BK>
 __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
   using namespace glds;
+  if (gemm_skipped(g)) return;
   static_assert(NS >= 2 && NS <= 5, "stages");
   static_assert(BK == 8 || BK == 16, "slice depth");
   constexpr int SA = Geo<BK>::SA, STAGE = Geo<BK>::STAGE, PIECES = Geo<BK>::PIECES;
@@ -674,6 +686,7 @@ __device__ __forceinline__ void wait_slices(int n) {  // the pieces of the n new
 template <int MODE, int NS, int OCC, int BK>
 __global__ __launch_bounds__(glds32::NT, OCC) void gemm_glds_f32(GemmArgs g) {
   using namespace glds32;
+  if (gemm_skipped(g)) return;
   static_assert(NS >= 2 && NS <= 4, "stages");
   static_assert(BK == 8 || BK == 16 || BK == 32, "slice depth");
   constexpr int SA = BK * BM, SB = BK * BN, STAGE = SA + SB;
@@ -922,6 +935,9 @@ static void fill_extra(GemmArgs& a, const GemmExtra* ex) {
   a.tneg = ex ? ex->tneg : nullptr;
   a.ldt = ex ? ex->ldtneg : 0;
   a.tncols = (ex && ex->tneg_cols > 0) ? ex->tneg_cols : (int64_t(1) << 62);
+  a.pred = ex ? ex->owner_phys : nullptr;
+  a.pred_p = ex ? ex->owner_p : 1;
+  a.pred_k = ex ? ex->owner_k : 0;
 }
 
 void gemm(DType dt, int op, int a_kmajor, int64_t M, int64_t N, int64_t K, const void* A,

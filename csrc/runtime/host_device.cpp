@@ -49,6 +49,10 @@ const T* tp(const void* p) {
 template <typename T>
 void gemm_t(GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const T* A, int64_t lda,
             const T* B, int64_t ldb, T* C, int64_t ldc, int nthreads, const GemmExtra& ex) {
+  if (ex.owner_phys) {  // owner-predicated (GemmExtra::owner_phys)
+    const int64_t g = *ex.owner_phys;
+    if (g < 0 || g % ex.owner_p != ex.owner_k) return;
+  }
   parallel_for(M, nthreads, [&](int64_t i) {
     bool zrow = false;
     for (int z = 0; z < ex.nzr; ++z) zrow |= (i >= ex.zr[z] && i < ex.zr[z] + ex.zh);

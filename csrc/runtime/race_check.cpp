@@ -365,6 +365,7 @@ void gemm_acc(std::vector<Acc>& a, DType dt, GemmOp op, ALayout al, int64_t M, i
     const int64_t cols = ex.tneg_cols > 0 ? std::min(ex.tneg_cols, N) : N;
     a.push_back(W(rect(ex.tneg, ex.ldtneg, M, cols, es), "tneg"));
   }
+  if (ex.owner_phys) a.push_back(R(span(ex.owner_phys, 4), "owner"));
 }
 
 }  // namespace

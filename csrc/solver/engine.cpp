@@ -724,6 +724,11 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
     void* pp = elem(PP_[par], j * m * dm);
     GemmExtra lat;
     lat.latency = true;
+    if (ahead && L_.p > 1) {  // enqueued on every rank, executed by the pivot's owner only
+      lat.owner_phys = seq_ + t;
+      lat.owner_p = L_.p;
+      lat.owner_k = L_.k;
+    }
     if (owner) {
       // RP = the pivot row over the panel's columns before normalisation, in one batched launch:
       //   earlier pivot columns jc < j: the sum over steps jc..j-1 only (no input),
@@ -748,6 +753,11 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
           g.B = elem(PP_[par], (j + 1) * m); g.ldb = dm;
           g.C = elem(RP_, (j + 1) * m); g.ldc = dm;
         }
+      }
+      for (int i = 0; i < np; ++i) {
+        pr[i].ex.owner_phys = lat.owner_phys;
+        pr[i].ex.owner_p = lat.owner_p;
+        pr[i].ex.owner_k = lat.owner_k;
       }
       dev_.gemm_batch(opt_.dtype, pr, np, S_SIDE);
       dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, q * m, m, Ht_[par][j], m, RP_, dm, pp,

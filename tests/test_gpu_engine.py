@@ -235,3 +235,18 @@ def test_race_check_on_gpu(p):
     assert rep["race_ops"] > 0
     assert rep["race_count"] == 0, "\n".join(rep["races"])
     assert rep["residual"] < 1e-8
+
+
+@pytest.mark.parametrize("p", [2, 4])
+def test_host_free_chain_multi_rank_on_one_gpu(p, monkeypatch):
+    """GJ_HOST_FREE=1 at p > 1 on the GPU: owner-predicated piece GEMMs (GemmExtra::owner_phys),
+    device-addressed owner edits, panel pieces by all-reduce.  Bit-identical to the host-driven
+    chain on the same stream-ordered virtual ranks."""
+    n, m = 1500, 64
+    A = generate_matrix(n, "random", 9)[::-1].copy()
+    ref = gj.GaussJordan(block_size=m, ranks=p, device="gpu", comm="async", depth=4, chunk_cols=256).inverse(A)
+    monkeypatch.setenv("GJ_HOST_FREE", "1")
+    got = gj.GaussJordan(block_size=m, ranks=p, device="gpu", comm="async", jitter_us=30.0, depth=4,
+                         chunk_cols=256).inverse(A)
+    assert np.array_equal(got, ref)
+    assert np.abs(got - np.linalg.inv(A)).max() / np.abs(ref).max() < 1e-8
