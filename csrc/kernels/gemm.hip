@@ -647,7 +647,21 @@ static void launch_glds(const GemmArgs& a0, hipStream_t s) {
   // the <2,3,8> schedule is the faster of the two 4-per-CU builds, so it is the only build.  Tile
   // rows are walked in groups of 4 (+0.5-1 %; groups 1-32 measured).
   a.group = 4;
-  hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 3, 8>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
+  // GJ_GLDS_BUILD=<stages>.<waves-per-SIMD bound>: in-solve re-measurement of the residency trade
+  // (the pivot chain got lighter in round 4: no dead candidate-inverse workgroups, no host round
+  // trip per step); 2.3 is the default build
+  static const int build = [] {
+    const char* e = getenv("GJ_GLDS_BUILD");
+    if (!e) return 23;
+    const std::string v = e;
+    return v == "2.5" ? 25 : v == "3.3" ? 33 : 23;
+  }();
+  if (build == 25)
+    hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 5, 8>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
+  else if (build == 33)
+    hipLaunchKernelGGL((gemm_glds_f64<MODE, 3, 3, 8>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 3, 8>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
 }
 
 static bool glds_ok(const GemmArgs& a) {

@@ -15,3 +15,11 @@ for n in 8192 16384 32768; do
     done
   done
 done
+# in-solve residency trade of the trailing-update GEMM, re-measured after the chain got lighter
+for b in 2.3 2.5 3.3; do
+  GJ_GLDS_BUILD=$b timeout -k 10 240 python bench.py --steps 4 --warmup 2 --no-residual > $o/glds_$b.json 2>&1 || exit $?
+  python3 -c "import json; d=json.loads(open('$o/glds_$b.json').read().splitlines()[-1]); print('glds $b', d['ms_per_step'])"
+  GJ_GLDS_BUILD=$b timeout -k 10 120 python bench.py --size 16384 --steps 8 --warmup 2 --no-residual > $o/glds16k_$b.json 2>&1 || exit $?
+  python3 -c "import json; d=json.loads(open('$o/glds16k_$b.json').read().splitlines()[-1]); print('glds16k $b', d['ms_per_step'])"
+done
+bash scripts/gemm_stall_pmc.sh
