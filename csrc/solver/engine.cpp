@@ -640,8 +640,8 @@ void Engine::begin_panel(int64_t v) {
   cur_phase_ = "pivot search";
   dev_.wait(S_SIDE, ev_L_);
   // this panel's steps rewrite Lrow_ / Ht_ / PP_[v & 1], which the COMM chunk pass of panel v - 2
-  // reads (with the look-ahead update on SIDE nothing else orders the two; the asynchronous
-  // virtual-rank test, tests/test_async_ranks.py, fails without this wait)
+  // reads; with the look-ahead update on SIDE nothing else orders the two (the happens-before
+  // checker reports Ht / Lrow / PP conflicts without this wait: tests/test_race_check.py "cp")
   if (v >= 2 && !dropped("cp")) dev_.wait(S_SIDE, ev_cp_[v & 1]);
   select(panel_t0(v), At_[v % 3]);
 }
