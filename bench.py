@@ -184,9 +184,7 @@ def run_rank(args) -> int:
 
         from mpi_jordan_crazy_acceleration_amd.utils import rccl_log as _rl
 
-        path = os.path.join(tempfile.gettempdir(), f"gj_rccl_{os.getpid()}.log")
-        if _rl.enable(path):
-            rccl_log = path
+        rccl_log = _rl.enable(os.path.join(tempfile.gettempdir(), f"gj_rccl_{os.getpid()}.log"))
     if args.bcast:
         os.environ["GJ_BCAST"] = args.bcast
     from datetime import timedelta

@@ -16,16 +16,20 @@ from typing import Optional
 _VIA = re.compile(r"Channel \d+/\d+ ?: .*?\bvia\s+([A-Za-z0-9_]+(?:/[A-Za-z0-9_]+)?)")
 
 
-def enable(path: str, environ=None) -> bool:
-    """Route RCCL's INFO log of the connection setup to `path` unless the user configured NCCL_DEBUG.
-    Must run before the process's first RCCL call."""
+def enable(path: str, environ=None) -> Optional[str]:
+    """Route RCCL's INFO log of the connection setup to a file; returns the file to parse (None:
+    the user already sends an INFO log to a file of their own naming, which is left alone).  A
+    quieter NCCL_DEBUG (WARN, as images often set) is raised to INFO for this process: the
+    connection lines are only logged at INFO.  Must run before the process's first RCCL call."""
     env = os.environ if environ is None else environ
-    if env.get("NCCL_DEBUG"):
-        return False
-    env["NCCL_DEBUG"] = "INFO"
-    env["NCCL_DEBUG_SUBSYS"] = "INIT,P2P,NET"
+    level = env.get("NCCL_DEBUG", "").upper()
+    if level in ("INFO", "TRACE") and env.get("NCCL_DEBUG_FILE"):
+        return None
+    if level not in ("INFO", "TRACE"):
+        env["NCCL_DEBUG"] = "INFO"
+        env["NCCL_DEBUG_SUBSYS"] = "INIT,P2P,NET"
     env["NCCL_DEBUG_FILE"] = path
-    return True
+    return path
 
 
 def transports(path: Optional[str]) -> Optional[dict]:

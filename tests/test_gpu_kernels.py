@@ -429,7 +429,9 @@ def test_block_inverse_live_grid_matches_full_grid(native, variant, m, dtype, p,
     finally:
         native.set_block_inverse_variant("panel")
     assert torch.equal(valid[live], full[2][live])
-    assert torch.equal(scores[live], full[1][live])
+    # the register-sweep kernel sums ||inv|| with atomics (order-dependent last bits); the inverses
+    # themselves are bit-identical
+    assert torch.allclose(scores[live], full[1][live], rtol=1e-13, atol=0)
     assert torch.equal(inv_t[live], full[0][live])
     dead = np.flatnonzero(mine != 0)
     assert torch.equal(valid[dead], sentinel[2][dead]) and torch.equal(inv_t[dead], sentinel[0][dead])
