@@ -56,6 +56,10 @@ struct GemmExtra {
   // rank owns the pivot g = *owner_phys (g % owner_p == owner_k) -- read on the device.
   const int32_t* owner_phys = nullptr;
   int64_t owner_p = 1, owner_k = 0;
+  // Trailing-update residency: 5 LDS-DMA workgroups per CU instead of 4 (a 96-VGPR build).  Faster
+  // when the pivot chain has CUs of its own (a CU reservation), slower when it must share them
+  // (profiles/gemm_stall_r4.md).
+  bool dense = false;
 };
 
 // Owner-side piece work fused into Device::owner_edits (all optional; w = 0 / eye = null: none):

@@ -167,6 +167,7 @@ class Engine {
     int reserve_cus = 0;          // CUs kept off the trailing-update stream
     std::string block_inverse;    // candidate-inverse kernel
     bool comm_small_tiles = false;
+    bool dense_gemm = false;      // trailing update at 5 workgroups per CU
     std::string pivot;            // "block-min-inv-norm" | "partial"
   };
   Policy policy() const;
@@ -242,6 +243,7 @@ class Engine {
   bool comm_small_tiles_ = false;  // COMM chunk-normalisation GEMMs on the small latency tile
   int bi_hint_ = -1;               // candidate-inverse kernel family (Device::set_block_inverse_hint)
   int reserved_cus_ = 0;
+  bool dense_gemm_ = false;  // trailing update at 5 workgroups per CU (GemmExtra::dense)
   double norm_a_ = -1;
 
   // chunk plan (block-column ranges, multiples of d_ blocks so a panel never straddles chunks)

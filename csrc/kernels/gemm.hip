@@ -144,6 +144,7 @@ struct GemmArgs {
   int64_t ldt, tncols;
   const int32_t* pred;  // GemmExtra::owner_phys: skip unless *pred % pred_p == pred_k
   int64_t pred_p, pred_k;
+  bool dense;           // GemmExtra::dense: the 5-workgroups-per-CU LDS-DMA build
 };
 
 // GemmExtra::owner_phys: the whole launch is a no-op on ranks that do not own the pivot
@@ -650,12 +651,13 @@ static void launch_glds(const GemmArgs& a0, hipStream_t s) {
   // GJ_GLDS_BUILD=<stages>.<waves-per-SIMD bound>: in-solve re-measurement of the residency trade
   // (the pivot chain got lighter in round 4: no dead candidate-inverse workgroups, no host round
   // trip per step); 2.3 is the default build
-  static const int build = [] {
+  static const int forced = [] {
     const char* e = getenv("GJ_GLDS_BUILD");
-    if (!e) return 23;
+    if (!e) return 0;
     const std::string v = e;
     return v == "2.5" ? 25 : v == "3.3" ? 33 : 23;
   }();
+  const int build = forced ? forced : (a.dense ? 25 : 23);
   if (build == 25)
     hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 5, 8>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
   else if (build == 33)
@@ -952,6 +954,7 @@ static void fill_extra(GemmArgs& a, const GemmExtra* ex) {
   a.pred = ex ? ex->owner_phys : nullptr;
   a.pred_p = ex ? ex->owner_p : 1;
   a.pred_k = ex ? ex->owner_k : 0;
+  a.dense = ex ? ex->dense : false;
 }
 
 void gemm(DType dt, int op, int a_kmajor, int64_t M, int64_t N, int64_t K, const void* A,

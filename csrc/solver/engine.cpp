@@ -133,6 +133,8 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // the reservation at 100 GB/s, p = 2 / 4 are 9 / 6 % slower (profiles/cu_reserve_pgt1.md).
   if (rc < 0) rc = (dev_.on_gpu() && (L_.npad <= 16384 || small_rank)) ? 32 : 0;
   reserved_cus_ = dev_.reserve_cus(rc);
+  dense_gemm_ = reserved_cus_ > 0;
+  if (const char* e = std::getenv("GJ_DENSE_GEMM")) dense_gemm_ = std::atoi(e) != 0;
   // Candidate inverses on ranks whose trailing update holds every CU (p > 1 without a reservation:
   // the 16384- and 8192-row ranks of N = 32768) take the co-resident 4-wave form, which starts in
   // the slot one retiring trailing-update workgroup frees instead of waiting for a whole CU: the
@@ -207,6 +209,7 @@ Engine::Policy Engine::policy() const {
   p.reserve_cus = reserved_cus_;
   p.block_inverse = dev_.on_gpu() ? kern::block_inverse_kernel_name(opt_.dtype, L_.m, bi_hint_) : "host";
   p.comm_small_tiles = comm_small_tiles_;
+  p.dense_gemm = dense_gemm_;
   p.pivot = opt_.pivot == PivotRule::Partial ? "partial" : "block-min-inv-norm";
   return p;
 }
@@ -1047,6 +1050,10 @@ void Engine::big_update(int64_t u) {
         GemmExtra ex = prows;
         ex.zc0 = pc0 - ra[z];  // the panel's own block columns enter as 0
         ex.zc1 = pc1 - ra[z];
+        // with CUs reserved for the pivot chain the trailing update may fill the rest densely:
+        // N = 16384 161.6 vs 164.6 ms; without a reservation the chain starves (N = 32768 1195 vs
+        // 1158 ms), profiles/gemm_stall_r4.md
+        ex.dense = dense_gemm_;
         dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, rb[z] - ra[z], K, At, rows,
                   rb_chunk(par, c) + (ra[z] - c0) * (int64_t)esz(), W, elem(X_, ra[z]), npad, ms, ex);
       }
