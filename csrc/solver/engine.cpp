@@ -98,6 +98,8 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // inverse (profiles/depth_pgt1.md) that the happens-before checker (race_check.hpp) does not
   // explain -- the schedule matrix of tests/test_race_check.py is race-free -- so p > 1 keeps the
   // depth the multi-rank tests and the scaling runs have always used.
+  // (One GPU at N = 32768, depth 8 with the co-resident candidate inverse: 0.9 % faster on one box,
+  // 0.5-0.8 % slower on another, same-box A/Bs of round 4 -- not adopted, profiles/rocprof_n32768_r4.md.)
   const int want = opt_.depth > 0 ? opt_.depth
                                   : (L_.p == 1 && L_.npad <= 8192) ? 2 : (small_rank && L_.npad > 16384) ? 8 : 4;
   d_ = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)want, (int64_t)kMaxDepth, L_.Nr}));

@@ -34,6 +34,19 @@ def main(db, title=""):
         by[r[5]][1] += r[2]
     for s, v in sorted(by.items()):
         print(f"| {s} | {v[0]} | {v[1]/1e6:.1f} | {100*v[1]/1e6/span:.1f} |")
+    print("\n## By kernel (all grid sizes together)\n")
+    print("| kernel | streams | calls | total ms | avg us | workgroups per call | % |")
+    print("|---|---|---|---|---|---|---|")
+    kn = collections.defaultdict(lambda: [0, 0.0, 0, set()])
+    for r in rows:
+        a = kn[r[0].split("(")[0][:70]]
+        a[0] += 1
+        a[1] += r[2]
+        a[2] += r[1]
+        a[3].add(r[5])
+    for name, v in sorted(kn.items(), key=lambda x: -x[1][1])[:16]:
+        st = ",".join(str(x) for x in sorted(v[3]))
+        print(f"| `{name}` | {st} | {v[0]} | {v[1]/1e6:.2f} | {v[1]/v[0]/1e3:.1f} | {v[2]/v[0]:.1f} | {100*v[1]/tot:.1f} |")
 
 
 if __name__ == "__main__":
