@@ -192,6 +192,12 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // but N = 16384 +1.1 % and N = 32768 +0.7 % (more COMM workgroups beside the trailing update), so
   // only where the pivot chain dominates (padded order <= 8192).  GJ_COMM_SMALL_TILES overrides.
   comm_small_tiles_ = L_.npad <= 8192;
+  // Look-ahead rows on SIDE, right behind the panel pieces, at every p (GJ_LA_SIDE=0 puts them on
+  // COMM at p = 1, round 3's one-rank choice): with the host-free pivot chain, COMM's queue (the
+  // previous panel's chunk pass, waiting for MAIN) is what held them back.  Round 4, same box,
+  // two repetitions: N = 8192 26.71 / 26.73 -> 25.73 / 25.80 ms; N = 16384 and 32768 neutral.
+  la_side_ = true;
+  if (const char* e = std::getenv("GJ_LA_SIDE")) la_side_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("GJ_HOST_FREE")) host_free_multi_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("GJ_COMM_SMALL_TILES")) comm_small_tiles_ = std::atoi(e) != 0;
 
@@ -832,10 +838,10 @@ void Engine::lookahead_rows(int64_t v, bool wait_main) {
   cur_phase_ = "look-ahead rows";
   if (v + 1 < npanels()) {
     const int64_t xa = panel_t0(v + 1) * m, wla = panel_q(v + 1) * m;
-    // at p > 1 on SIDE, right behind the panel pieces, with SIDE's communicator: emulated N = 16384
-    // p = 4 at 50 GB/s per link 0.0588 -> 0.0564 s (80 % of the transfer hidden), p = 8 0.0430 ->
-    // 0.0425 s; one rank keeps it on COMM (N = 8192 28.66 vs 28.84 ms) -- profiles/emu_direct_r3.md
-    const bool la_side = L_.p > 1;
+    // on SIDE, right behind the panel pieces, with SIDE's communicator: emulated N = 16384 p = 4 at
+    // 50 GB/s per link 0.0588 -> 0.0564 s (80 % of the transfer hidden), p = 8 0.0430 -> 0.0425 s
+    // (profiles/emu_direct_r3.md); one rank too since round 4 (la_side_, constructor)
+    const bool la_side = la_side_;
     const int ls = la_side ? S_SIDE : S_COMM;
     void* Tl = la_side ? T2_ : T_;
     if (!la_side) dev_.wait(S_COMM, ev_pp_[par][q - 1]);  // panel pieces, Lrow, H_t (SIDE)
