@@ -168,6 +168,7 @@ class Engine {
     std::string block_inverse;    // candidate-inverse kernel
     bool comm_small_tiles = false;
     bool dense_gemm = false;      // trailing update at 5 workgroups per CU
+    bool la_side = true;          // look-ahead rows on SIDE (else COMM)
     std::string pivot;            // "block-min-inv-norm" | "partial"
   };
   Policy policy() const;

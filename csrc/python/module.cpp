@@ -447,6 +447,7 @@ PYBIND11_MODULE(_C, mod) {
                                d["block_inverse"] = pl.block_inverse;
                                d["comm_small_tiles"] = pl.comm_small_tiles;
                                d["dense_gemm"] = pl.dense_gemm;
+                               d["look_ahead_rows"] = pl.la_side ? "SIDE" : "COMM";
                                d["pivot"] = pl.pivot;
                                d["bcast"] = e.eng->bcast_algo();
                                d["bcast_tuning"] = e.comm->bcast_report();

@@ -218,6 +218,7 @@ Engine::Policy Engine::policy() const {
   p.block_inverse = dev_.on_gpu() ? kern::block_inverse_kernel_name(opt_.dtype, L_.m, bi_hint_) : "host";
   p.comm_small_tiles = comm_small_tiles_;
   p.dense_gemm = dense_gemm_;
+  p.la_side = la_side_;
   p.pivot = opt_.pivot == PivotRule::Partial ? "partial" : "block-min-inv-norm";
   return p;
 }

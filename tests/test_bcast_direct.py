@@ -57,3 +57,17 @@ def test_tune_bcast_binding_single_rank(monkeypatch):
     comm = C.self_comm()
     assert comm.tune_bcast(C.host_device(1), 1 << 20) == "ring"
     assert comm.bcast_report() == "ring"
+
+
+def test_engine_policy_knobs(monkeypatch):
+    """The policy the engine reports follows its environment overrides (README "Runtime knobs"):
+    the dense trailing-update build is on exactly where CUs are reserved (none on the host
+    executor) unless GJ_DENSE_GEMM says otherwise; the look-ahead rows run on SIDE unless
+    GJ_LA_SIDE=0."""
+    C = gj.load_native()
+    pol = C.Engine(C.host_device(1), C.self_comm(), 64, 8, "fp64").policy
+    assert pol["dense_gemm"] is False and pol["reserve_cus"] == 0 and pol["look_ahead_rows"] == "SIDE"
+    monkeypatch.setenv("GJ_DENSE_GEMM", "1")
+    monkeypatch.setenv("GJ_LA_SIDE", "0")
+    pol = C.Engine(C.host_device(1), C.self_comm(), 64, 8, "fp64").policy
+    assert pol["dense_gemm"] is True and pol["look_ahead_rows"] == "COMM"
