@@ -22,3 +22,8 @@ for rep in 1 2; do
     done
   done
 done
+GJ_GLDS_PAIR=0 timeout -k 10 300 python bench/bench_emulate.py --ranks 8 --size 16384 --depth 2 4 --reps 2 --bw 50 --bcast direct > $o/emu_d.txt 2>&1 || exit $?
+grep '"seconds"' $o/emu_d.txt | python3 -c "
+import sys, json
+for l in sys.stdin:
+    d = json.loads(l); print('emu', d['p'], d['n'], d['depth'], d.get('bcast', 'free'), d['seconds'])"
