@@ -245,7 +245,8 @@ class Engine {
   int bi_hint_ = -1;               // candidate-inverse kernel family (Device::set_block_inverse_hint)
   int reserved_cus_ = 0;
   bool dense_gemm_ = false;
-  bool la_side_ = true;           // look-ahead rows on SIDE (else COMM); GJ_LA_SIDE overrides  // trailing update at 5 workgroups per CU (GemmExtra::dense)
+  bool la_side_ = true;
+  int bi_split_hint_ = -1;        // candidate-inverse family for steps with more live candidates than reserved CUs           // look-ahead rows on SIDE (else COMM); GJ_LA_SIDE overrides  // trailing update at 5 workgroups per CU (GemmExtra::dense)
   double norm_a_ = -1;
 
   // chunk plan (block-column ranges, multiples of d_ blocks so a panel never straddles chunks)

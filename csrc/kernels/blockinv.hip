@@ -815,9 +815,12 @@ size_t block_inverse_iscratch_bytes(const Layout& L) {
 
 bool block_inverse_select(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                           int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
-                          hipStream_t s, const PivotSelectArgs& sel, int variant) {
+                          hipStream_t s, const PivotSelectArgs& sel, int variant, void* scratch) {
   const int v = variant >= 0 ? variant : bi_variant();
-  if (v != 0 || L.nblk <= 0) return false;
+  if (L.nblk <= 0) return false;
+  if (v == 5)
+    return scratch && block_inverse_co(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, nlive, s, scratch, &sel);
+  if (v != 0) return false;
   return block_inverse_mfma(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, nlive, s, &sel);
 }
 

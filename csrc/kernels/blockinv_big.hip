@@ -28,6 +28,7 @@
 
 #include "kernels.hpp"
 #include "pivot_panel.hpp"
+#include "pivot_select.hpp"
 #include "wave_ops.hpp"
 
 namespace gj {
@@ -72,7 +73,8 @@ template <int MP, int NB, int LAY = 0>
 __global__ __launch_bounds__(64 * (NB + 1 + (LAY ? (NB - 1) / 3 : 0))) void block_inverse_l2_kernel(
     const double* __restrict__ Lt, int64_t ldl, double* __restrict__ inv_t, double* __restrict__ scores,
     int32_t* __restrict__ valid, const int32_t* __restrict__ used, int m, int64_t p, int64_t k,
-    double thresh, double* __restrict__ scratch, int32_t* __restrict__ piv_out, int live_nblk) {
+    double thresh, double* __restrict__ scratch, int32_t* __restrict__ piv_out, PivotSelectArgs sel,
+    int live_nblk) {
   constexpr int NT = MP / 16;               // tiles per dimension = panels
   constexpr int CPW = (NT + NB - 1) / NB;    // column tiles per block wave (ct = wave + NB j < NT)
   constexpr int RPL = MP / 64;               // pivot-wave rows per lane
@@ -80,11 +82,16 @@ __global__ __launch_bounds__(64 * (NB + 1 + (LAY ? (NB - 1) / 3 : 0))) void bloc
   constexpr int RWC = 16 * CPW + 1;
   static_assert(MP % 64 == 0 && NB <= NT && 2 * LDU >= NB, "geometry");
 
+  // the fused selection (select_tail, one whole wave per workgroup) as in blockinv_mfma.hip
+  const int nblk = live_nblk ? live_nblk : (int)gridDim.x;
   const int b = live_nblk ? live_block(used, live_nblk, p, k) : (int)blockIdx.x;  // see live_block
   if (b < 0 || used[(int64_t)b * p + k]) {
-    if (threadIdx.x == 0 && b >= 0) {
-      valid[b] = 0;
-      scores[b] = 0.0;
+    if (threadIdx.x < 64) {
+      if (threadIdx.x == 0 && b >= 0) {
+        valid[b] = 0;
+        scores[b] = 0.0;
+      }
+      select_tail(sel, scores, valid, used, nblk, p, k);
     }
     return;
   }
@@ -180,6 +187,7 @@ __global__ __launch_bounds__(64 * (NB + 1 + (LAY ? (NB - 1) / 3 : 0))) void bloc
       valid[b] = 0;
       scores[b] = 0.0;
     }
+    select_tail(sel, scores, valid, used, nblk, p, k);
     return;
   }
 
@@ -311,25 +319,28 @@ bool block_inverse_big(DType dt, const void* Lt, int64_t ldl, void* inv_t, doubl
   // the pivot wave alone on its SIMD (11-wave layout): -6 to -7 % per batch against the 9-wave one
   hipLaunchKernelGGL((block_inverse_l2_kernel<256, 8, 1>), dim3(grid), dim3(64 * 11), 0, s,
                      static_cast<const double*>(Lt), ldl, static_cast<double*>(inv_t), scores, valid, used, m,
-                     L.p, L.k, thresh, static_cast<double*>(scratch), block_inverse_probe(), live_nblk);
+                     L.p, L.k, thresh, static_cast<double*>(scratch), block_inverse_probe(), PivotSelectArgs{},
+                     live_nblk);
   return true;
 }
 
 bool block_inverse_co(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,
-                      const int32_t* used, const Layout& L, double thresh, int64_t nlive, hipStream_t s, void* scratch) {
+                      const int32_t* used, const Layout& L, double thresh, int64_t nlive, hipStream_t s, void* scratch,
+                      const PivotSelectArgs* sel) {
   const int m = (int)L.m;
   if (dt != DType::F64 || m <= 32 || m > 128) return false;
   if (L.nblk == 0) return true;
   const unsigned grid = (unsigned)(nlive >= 0 ? std::max<int64_t>(nlive, 1) : L.nblk);
   const int live_nblk = nlive >= 0 ? (int)L.nblk : 0;
+  const PivotSelectArgs tail = sel ? *sel : PivotSelectArgs{};
   if (m <= 64)
     hipLaunchKernelGGL((block_inverse_l2_kernel<64, 3>), dim3(grid), dim3(64 * 4), 0, s,
                        static_cast<const double*>(Lt), ldl, static_cast<double*>(inv_t), scores, valid, used, m,
-                       L.p, L.k, thresh, static_cast<double*>(scratch), block_inverse_probe(), live_nblk);
+                       L.p, L.k, thresh, static_cast<double*>(scratch), block_inverse_probe(), tail, live_nblk);
   else
     hipLaunchKernelGGL((block_inverse_l2_kernel<128, 3>), dim3(grid), dim3(64 * 4), 0, s,
                        static_cast<const double*>(Lt), ldl, static_cast<double*>(inv_t), scores, valid, used, m,
-                       L.p, L.k, thresh, static_cast<double*>(scratch), block_inverse_probe(), live_nblk);
+                       L.p, L.k, thresh, static_cast<double*>(scratch), block_inverse_probe(), tail, live_nblk);
   return true;
 }
 

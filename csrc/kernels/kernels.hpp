@@ -48,7 +48,7 @@ bool block_inverse_mfma(DType dt, const void* Lt, int64_t ldl, void* inv_t, doub
 // launched, the caller runs block_inverse and the selection separately
 bool block_inverse_select(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                           int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
-                          hipStream_t s, const PivotSelectArgs& sel, int variant = -1);
+                          hipStream_t s, const PivotSelectArgs& sel, int variant = -1, void* scratch = nullptr);
 // test probe: when set, the matrix-core block inverses write the pivot row of every column of
 // every candidate to piv_out[b * m + c] (device memory; nullptr = off)
 void set_block_inverse_probe(int32_t* piv_out);
@@ -57,9 +57,11 @@ int32_t* block_inverse_probe();
 bool block_inverse_big(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,
                        const int32_t* used, const Layout& L, double thresh, int64_t nlive, hipStream_t s, void* scratch);
 size_t block_inverse_big_scratch_bytes(DType dt, const Layout& L);
-// the co-resident form (4 waves, fits the slot one trailing-update workgroup frees): fp64 32 < m <= 128
+// the co-resident form (4 waves, fits the slot one trailing-update workgroup frees): fp64 32 < m <= 128;
+// with sel, the batch's last workgroup also runs the selection (as block_inverse_mfma)
 bool block_inverse_co(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,
-                      const int32_t* used, const Layout& L, double thresh, int64_t nlive, hipStream_t s, void* scratch);
+                      const int32_t* used, const Layout& L, double thresh, int64_t nlive, hipStream_t s, void* scratch,
+                      const PivotSelectArgs* sel = nullptr);
 // scratch needed by the fp64 m > 128 paths (big kernel / generic sweep)
 // (variant: the kernel family to use for this call, -1 = the process-wide setting)
 size_t block_inverse_scratch_bytes(DType dt, const Layout& L, int variant = -1);

@@ -252,8 +252,11 @@ void HipDevice::block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t
 bool HipDevice::block_inverse_select(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,
                                      int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
                                      const PivotSelectArgs& sel, int s) {
+  const int variant = bi_hint_;
+  const size_t b1 = kern::block_inverse_scratch_bytes(dt, L, variant);
+  void* sc = b1 ? scratch(b1, 0) : nullptr;
   if (!kern::block_inverse_select(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, nlive, hs(streams_[s]), sel,
-                                  bi_hint_))
+                                  variant, sc))
     return false;
   check_launch();
   return true;

@@ -27,3 +27,9 @@ grep '"seconds"' $o/emu_d.txt | python3 -c "
 import sys, json
 for l in sys.stdin:
     d = json.loads(l); print('emu', d['p'], d['n'], d['depth'], d.get('bcast', 'free'), d['seconds'])"
+for rep in 1 2; do
+  for cc in 8192 16384 32768; do
+    timeout -k 10 200 python bench.py --chunk-cols $cc --steps 3 --warmup 1 --no-residual > $o/cc.json 2>&1 || exit $?
+    python3 -c "import json; d=json.loads(open('$o/cc.json').read().splitlines()[-1]); print('chunk_cols=$cc', d['ms_per_step'], d['policy']['nchunks'])"
+  done
+done
