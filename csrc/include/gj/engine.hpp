@@ -19,10 +19,12 @@
 //     pieces", d*m x d*m) so that the big GEMM needs only zero-column / zero-row masks (GemmExtra)
 //     and no special rows inside the hot kernel.  d = 4 gives K = 512 at m = 128.
 //   * Look-ahead (three HIP streams): MAIN runs the big update of panel u; SIDE (high priority)
-//     first updates the next panel's columns, then runs its pivot searches (batched in-register
+//     first forms and broadcasts panel u's pivot rows over the next panel's columns (look-ahead
+//     rows), updates those columns, then runs the next panel's pivot searches (batched in-register
 //     block inverses + RCCL all-gather of 32-B PivotRec + deterministic argmin on device) and the
-//     narrow edits; COMM normalises the next panel's pivot rows and broadcasts them chunk by chunk
-//     (one event per chunk) so MAIN's next update can start on chunk 0 while chunk k is in flight.
+//     narrow edits; COMM normalises panel u's pivot rows over the rest of the columns and
+//     broadcasts them chunk by chunk (one event per chunk) so MAIN's update can start on chunk 0
+//     while chunk k is in flight.  Every cross-stream edge is checked by RaceCheckDevice.
 #pragma once
 
 #include <algorithm>
