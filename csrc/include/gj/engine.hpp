@@ -246,9 +246,8 @@ class Engine {
   bool comm_small_tiles_ = false;  // COMM chunk-normalisation GEMMs on the small latency tile
   int bi_hint_ = -1;               // candidate-inverse kernel family (Device::set_block_inverse_hint)
   int reserved_cus_ = 0;
-  bool dense_gemm_ = false;
-  bool la_side_ = true;
-  int bi_split_hint_ = -1;        // candidate-inverse family for steps with more live candidates than reserved CUs           // look-ahead rows on SIDE (else COMM); GJ_LA_SIDE overrides  // trailing update at 5 workgroups per CU (GemmExtra::dense)
+  bool dense_gemm_ = false;        // trailing update at 5 workgroups per CU (GemmExtra::dense)
+  bool la_side_ = true;            // look-ahead rows on SIDE (else COMM); GJ_LA_SIDE overrides
   double norm_a_ = -1;
 
   // chunk plan (block-column ranges, multiples of d_ blocks so a panel never straddles chunks)

@@ -449,13 +449,9 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, double* lds_wave
 // flight (P pieces per slice)
 template <int P>
 __device__ __forceinline__ void wait_pieces(int n) {
-  static_assert(P == 3 || P == 4 || P == 6, "pieces per slice");
+  static_assert(P == 3 || P == 6, "pieces per slice");
   if (n <= 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  } else if constexpr (P == 4) {
-    if (n == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if (n == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   } else if constexpr (P == 3) {
     if (n == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     else if (n == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
@@ -668,180 +664,6 @@ static void launch_glds(const GemmArgs& a0, hipStream_t s) {
     hipLaunchKernelGGL((gemm_glds_f64<MODE, 3, 3, 8>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
   else
     hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 3, 8>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
-}
-
-// ---- (experiment, GJ_GLDS_PAIR) 64 x 64 tile of 2 waves (64 x 32 each): the barrier joins two
-// waves instead of four.  A and B images [k][64], odd rows' 16-double halves swapped (no pad, so one
-// LDS-DMA piece covers two k rows); four pieces per wave per 8-deep slice.
-namespace gldsp {
-constexpr int BM = 64, BN = 64, NT = 128, BK = 8;
-constexpr int SA = BK * BM, SB = BK * BN, STAGE = SA + SB;
-}  // namespace gldsp
-
-template <int MODE, int NS, int OCC>
-__global__ __launch_bounds__(gldsp::NT, OCC) void gemm_glds_p_f64(GemmArgs g) {
-  using namespace gldsp;
-  if (gemm_skipped(g)) return;
-  using MF = Mfma<double>;
-  using acc_t = MF::acc_t;
-  constexpr int ES = 8, TN = 32, MI = 4, NJ = 2;
-  __shared__ double lds[NS * STAGE];
-
-  const int nwg = g.tiles_m * g.tiles_n;
-  const int tile = xcd_remap((int)blockIdx.x, nwg);
-  const int G = g.group > 0 ? g.group : 1;
-  const int grp = tile / (G * g.tiles_n), gr0 = grp * G;
-  const int gsz = (g.tiles_m - gr0) < G ? (g.tiles_m - gr0) : G;
-  const int rem = tile - grp * G * g.tiles_n;
-  const int tm = gr0 + rem % gsz, tn = rem / gsz;
-  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wid;
-  const double* A = static_cast<const double*>(g.A);
-  const double* B = static_cast<const double*>(g.B);
-  double* C = static_cast<double*>(g.C);
-  const int ldc = (int)g.ldc, ldb = (int)g.ldb, lda = (int)g.lda;
-
-  const int rlane = MF::rl(lane);
-  const int clane = wn * TN + (lane & 15);
-  const int Mt = (int)((g.M - m0) < BM ? (g.M - m0) : BM);
-  const int Nt = (int)((g.N - n0) < BN ? (g.N - n0) : BN);
-  const int64_t zlo = g.zc0 - n0, zhi = g.zc1 - n0;
-  const int z0 = (int)(zlo < 0 ? 0 : (zlo > BN ? BN : zlo)), z1 = (int)(zhi < 0 ? 0 : (zhi > BN ? BN : zhi));
-  int zr0[GemmExtra::kMaxZeroRows], zr1[GemmExtra::kMaxZeroRows];
-#pragma unroll
-  for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) {
-    const int64_t lo = g.zr[z] - m0, hi = g.zr[z] + g.zh - m0;
-    zr0[z] = (int)(lo < 0 ? 0 : (lo > BM ? BM : lo));
-    zr1[z] = (int)(hi < 0 ? 0 : (hi > BM ? BM : hi));
-  }
-  __amdgpu_buffer_rsrc_t rc = rsrc(C + m0 * g.ldc + n0);
-  const int cvoff = (rlane * ldc + clane) * ES;
-
-  acc_t acc[MI][NJ];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = rlane + i * 16 + MF::rq(q);
-      const int soff = (i * 16 + MF::rq(q)) * ldc * ES;
-      bool zrow = false;
-#pragma unroll
-      for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) zrow |= (r >= zr0[z] && r < zr1[z]);
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int c = clane + j * 16;
-        if (MODE == MODE_ACC) {
-          const bool ok = r < Mt && c < Nt && !zrow && !(c >= z0 && c < z1);
-          acc[i][j][q] = bload<double>(rc, ok ? cvoff + j * 16 * ES : kOOB, soff);
-        } else {
-          acc[i][j][q] = 0.0;
-        }
-      }
-    }
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) asm volatile("" ::"v"(acc[i][j][q]));
-
-  // piece h (0..1) of wave w: k rows 2 (2h + w) + (lane >> 5), columns 2 (lane & 31) of the image
-  const int pos = 2 * (lane & 31);
-  const int prow = 2 * wid + (lane >> 5);   // + 4 h
-  const int col = pos ^ ((prow & 1) * 16);
-  const bool a_ok = (m0 + col) < g.M;
-  const bool b_ok = (n0 + col) < g.N;
-  __amdgpu_buffer_rsrc_t ra = rsrc(A + m0);
-  __amdgpu_buffer_rsrc_t rb = rsrc(B + n0);
-  const int Kd = (int)g.K;
-  auto issue = [&](int kt) {
-    double* st = lds + (kt % NS) * STAGE;
-    const int k0 = kt * BK;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int kr = prow + 4 * h;
-      const bool okk = (k0 + kr) < Kd;
-      dma16(ra, st + (2 * wid + 4 * h) * BM, (a_ok && okk) ? ((k0 + kr) * lda + col) * ES : kOOB);
-      dma16(rb, st + SA + (2 * wid + 4 * h) * BN, (b_ok && okk) ? ((k0 + kr) * ldb + col) * ES : kOOB);
-    }
-  };
-  auto compute = [&](int kt) {
-    const double* sa = lds + (kt % NS) * STAGE;
-    const double* sb = sa + SA;
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += 4) {
-      double a[MI], b[NJ];
-      const int kr = kk + (lane >> 4);
-      const int sw = (kr & 1) * 16;
-#pragma unroll
-      for (int i = 0; i < MI; ++i) a[i] = sa[kr * BM + ((i * 16 + (lane & 15)) ^ sw)];
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) b[j] = sb[kr * BN + ((wn * TN + j * 16 + (lane & 15)) ^ sw)];
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = MF::op(a[i], b[j], acc[i][j]);
-    }
-  };
-
-  const int nk = (int)((g.K + BK - 1) / BK);
-  const int pro = nk < NS - 1 ? nk : NS - 1;
-  for (int kt = 0; kt < pro; ++kt) issue(kt);
-  wait_pieces<4>(pro - 1);
-  __builtin_amdgcn_s_barrier();
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + NS - 1 < nk) issue(kt + NS - 1);
-    compute(kt);
-    const int last = (kt + NS - 1 < nk ? kt + NS - 1 : nk - 1);
-    wait_pieces<4>(last - (kt + 1) > 0 ? last - (kt + 1) : 0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = rlane + i * 16 + MF::rq(q);
-      const int soff = (i * 16 + MF::rq(q)) * ldc * ES;
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int c = clane + j * 16;
-        bstore(acc[i][j][q], rc, (r < Mt && c < Nt) ? cvoff + j * 16 * ES : kOOB, soff);
-      }
-    }
-  if (g.tneg && n0 < g.tncols) {
-    __amdgpu_buffer_rsrc_t rt = rsrc(static_cast<double*>(g.tneg) + n0 * g.ldt + m0);
-    const int ldt = (int)g.ldt;
-    const int Ntn = (int)((g.tncols - n0) < Nt ? (g.tncols - n0) : Nt);
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int r = rlane + i * 16 + MF::rq(q);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int c = clane + j * 16;
-          bstore(-acc[i][j][q], rt, (r < Mt && c < Ntn) ? (c * ldt + r) * ES : kOOB, 0);
-        }
-      }
-  }
-}
-
-template <int MODE>
-static void launch_glds_p(const GemmArgs& a0, int build, hipStream_t s) {
-  GemmArgs a = a0;
-  a.tiles_m = (int)((a.M + gldsp::BM - 1) / gldsp::BM);
-  a.tiles_n = (int)((a.N + gldsp::BN - 1) / gldsp::BN);
-  const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;
-  if (nwg <= 0) return;
-  a.group = 8;
-  if (build == 3)
-    hipLaunchKernelGGL((gemm_glds_p_f64<MODE, 3, 4>), dim3((unsigned)nwg), dim3(gldsp::NT), 0, s, a);
-  else
-    hipLaunchKernelGGL((gemm_glds_p_f64<MODE, 2, 4>), dim3((unsigned)nwg), dim3(gldsp::NT), 0, s, a);
 }
 
 static bool glds_ok(const GemmArgs& a) {
@@ -1104,11 +926,6 @@ static void launch(const GemmArgs& a, hipStream_t s) {
   if (v == 11 && a.tneg && sizeof(T) == 4) v = 6;  // the fp32 LDS-DMA kernel has no -C^T epilogue
   if (v == 11) {  // LDS-DMA fp64 kernel; other dtypes / layouts / alignments take the next best tile
     if constexpr (sizeof(T) == 8 && AL == 1 && MODE != MODE_RESID) {
-      static const int pair = [] {
-        const char* e = getenv("GJ_GLDS_PAIR");
-        return e ? atoi(e) : 0;
-      }();
-      if (pair > 0 && glds_ok(a)) return launch_glds_p<MODE>(a, pair, s);
       if (glds_ok(a)) return launch_glds<MODE>(a, s);
     }
     if constexpr (sizeof(T) == 4 && AL == 1 && MODE != MODE_RESID) {

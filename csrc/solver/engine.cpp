@@ -151,11 +151,8 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
     if (const char* e = std::getenv("GJ_BI_CORESIDENT")) co = std::atoi(e) != 0;
     if (std::getenv("GJ_BI_VARIANT")) co = false;
     bi_hint_ = (co && fits) ? 5 : -1;
-    // (experiment, GJ_BI_SPLIT=1) with CUs reserved, a step whose live candidates outnumber them
-    // runs the register form in two rounds; the co-resident form fits two per CU: one round
-    if (reserved_cus_ > 0 && fits && bi_hint_ < 0)
-      if (const char* e = std::getenv("GJ_BI_SPLIT"))
-        if (std::atoi(e) != 0) bi_split_hint_ = 5;
+    // (Measured round 4: the co-resident form only for steps whose live candidates outnumber the
+    // reserved CUs -- two per CU, one round instead of two -- N = 8192 25.72 -> 27.36 ms: slower.)
   }
 
   comm_.set_timeout(opt_.comm_timeout_s);
@@ -245,9 +242,7 @@ int Engine::alloc_buffers(std::string& why) {
   const size_t need_work = 3 * (size_t)dm * rows * es + 2 * (size_t)dm * npad * es + 4 * (size_t)dm * dm * es +
                            (size_t)m * dm * es +
                            (size_t)std::max<int64_t>(L_.nblk, 1) * m * m * es + (size_t)m * wmax * es +
-                           std::max(dev_.block_inverse_scratch_bytes(opt_.dtype, L_, bi_hint_),
-                                    bi_split_hint_ >= 0 ? dev_.block_inverse_scratch_bytes(opt_.dtype, L_, bi_split_hint_)
-                                                        : size_t(0));
+                           dev_.block_inverse_scratch_bytes(opt_.dtype, L_, bi_hint_);
   const size_t avail = dev_.on_gpu() ? dev_.free_memory() : SIZE_MAX;
   auto fits = [&](size_t need) { return !dev_.on_gpu() || need + (64u << 20) <= avail; };
   // stage 1: the matrix panels (the reference's a / b arrays)
@@ -312,7 +307,6 @@ void Engine::alloc_work(int64_t wmax) {
   }
   // the candidate-inverse kernel's scratch, now: not lazily inside the first timed pivot search
   dev_.prepare_block_inverse(opt_.dtype, L_, bi_hint_);
-  if (bi_split_hint_ >= 0) dev_.prepare_block_inverse(opt_.dtype, L_, bi_split_hint_);
   scores_ = static_cast<double*>(dev_.alloc(sizeof(double) * std::max<int64_t>(L_.nblk, 1)));
   valid_ = static_cast<int32_t*>(dev_.alloc(sizeof(int32_t) * std::max<int64_t>(L_.nblk, 1)));
   pos_ = static_cast<int32_t*>(dev_.alloc(sizeof(int32_t) * L_.Nr));
@@ -598,8 +592,7 @@ void Engine::select(int64_t t, const void* Lt, bool full) {
     }
     bool fused = false;
     if (L_.nblk > 0) {
-      // per call: a device may be shared with other users
-      dev_.set_block_inverse_hint((bi_split_hint_ >= 0 && nlive > reserved_cus_) ? bi_split_hint_ : bi_hint_);
+      dev_.set_block_inverse_hint(bi_hint_);  // per call: a device may be shared with other users
       PivotSelectArgs sa;
       sa.done = sel_done_;
       sa.t = (int32_t)t;
