@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Record of a measurement: the switch it toggles was removed with the rejected variant; rerunning it
+# now measures the default twice.)
 # Incremental panel-column updates (GJ_INCR=1: rank-m update of the later panel columns after every
 # step, column t+1 on SIDE, the rest on AUX) against the per-step K = j*m column update.
 cd "$(dirname "$0")/.."

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Record of a measurement: the switch it toggles was removed with the rejected variant; rerunning it
+# now measures the default twice.)
 # 64 x 64 2-wave LDS-DMA tile (GJ_GLDS_PAIR=2) vs the default 128 x 64 4-wave tile.
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp

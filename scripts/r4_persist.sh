@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Record of a measurement: the switch it toggles was removed with the rejected variant; rerunning it
+# now measures the default twice.)
 # Resident-grid (persistent) LDS-DMA GEMM vs one workgroup per tile: alone and in the N = 32768 solve.
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp

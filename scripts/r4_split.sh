@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Record of a measurement: the switch it toggles was removed with the rejected variant; rerunning it
+# now measures the default twice.)
 # Co-resident candidate inverse with the fused selection: correctness (GPU engine tests with the
 # co-resident form forced, and with the per-step split), then N = 8192 / 16384 with GJ_BI_SPLIT=0/1
 # and the p = 2 / 4 ranks of N = 32768 (co-resident by default, now fused).

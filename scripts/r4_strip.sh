@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Record of a measurement: the switch it toggles was removed with the rejected variant; rerunning it
+# now measures the default twice.)
 # MAIN updates the panel-after-next's columns first (GJ_STRIP) and/or the look-ahead rows on SIDE at
 # p = 1 (GJ_LA_SIDE): same box, interleaved, two repetitions.
 cd "$(dirname "$0")/.."

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (Record of a measurement: the switch it toggles was removed with the rejected variant; rerunning it
+# now measures the default twice.)
 # 128 x 128 8-wave LDS-DMA tile (GJ_GLDS_WIDE=2/3 stages) vs the default 128 x 64 4-wave tile.
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
