@@ -148,3 +148,14 @@ def test_host_free_chain_multi_rank(p, depth, monkeypatch):
     got = gj.GaussJordan(block_size=20, ranks=p, device="cpu", comm="async", depth=depth,
                          host_threads=1).run(420, gen="random", seed=3, keep_inverse=True)
     assert np.array_equal(got["inverse"], ref["inverse"])
+
+
+@pytest.mark.parametrize("p", [1, 3])
+@pytest.mark.parametrize("depth", [2, 4])
+def test_look_ahead_rows_on_comm_race_free(p, depth, monkeypatch):
+    """GJ_LA_SIDE=0 (the round-3 one-rank schedule: look-ahead rows on COMM, behind the previous
+    panel's chunk pass) stays a supported knob: race-free and correct."""
+    monkeypatch.setenv("GJ_LA_SIDE", "0")
+    rep = _run(420, 20, p, depth=depth, chunk_cols=120)
+    assert rep["race_count"] == 0, "\n".join(rep["races"])
+    assert rep["residual"] < 1e-8
