@@ -191,8 +191,9 @@ PYBIND11_MODULE(_C, mod) {
            [](Device& d, const std::string& dt, const std::string& op, bool a_kmajor, int64_t M,
               int64_t N, int64_t K, U A, int64_t lda, U B, int64_t ldb, U C, int64_t ldc, int64_t zc0,
               int64_t zc1, std::vector<int64_t> zero_rows, int64_t zh, U tneg, int64_t ldtneg, bool latency,
-              int64_t tneg_cols) {
+              int64_t tneg_cols, bool dense) {
              GemmExtra ex;
+             ex.dense = dense;
              ex.tneg = (void*)tneg;
              ex.ldtneg = ldtneg;
              ex.tneg_cols = tneg_cols;
@@ -212,7 +213,7 @@ PYBIND11_MODULE(_C, mod) {
            py::arg("A"), py::arg("lda"), py::arg("B"), py::arg("ldb"), py::arg("C"), py::arg("ldc"),
            py::arg("zc0") = 0, py::arg("zc1") = 0, py::arg("zero_rows") = std::vector<int64_t>(),
            py::arg("zh") = 0, py::arg("tneg") = U(0), py::arg("ldtneg") = 0, py::arg("latency") = false,
-           py::arg("tneg_cols") = 0)
+           py::arg("tneg_cols") = 0, py::arg("dense") = false)
       .def("gemm_batch",
            [](Device& d, const std::string& dt,
               const std::vector<std::tuple<std::string, int64_t, int64_t, int64_t, U, int64_t, U, int64_t,

@@ -38,14 +38,15 @@ def _p(t: torch.Tensor) -> int:
 
 def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, op: str = "acc", a_kmajor: bool = False,
          zero_cols=(0, 0), zero_rows=(), zero_row_height: int = 0, tneg: torch.Tensor = None,
-         latency: bool = False) -> torch.Tensor:
+         latency: bool = False, dense: bool = False) -> torch.Tensor:
     """C += A@B (op="acc") or C = A@B (op="store").  With a_kmajor, ``A`` is given as A^T (K x M).
 
     Elimination extras (op="acc"): C enters as 0 in the columns ``zero_cols`` = (c0, c1) and in the
     row blocks [r, r + zero_row_height) for r in ``zero_rows`` (at most 8).  ``tneg`` (Nt x M view,
     Nt <= N, unit column stride): also receives -C^T of C's first Nt columns, the multiplier panel
     the engine's column / look-ahead updates write as they store C.  ``latency``: the small-tile
-    launch the pivot chain uses."""
+    launch the pivot chain uses.  ``dense``: the 5-workgroups-per-CU build of the fp64 LDS-DMA
+    trailing update (the engine's choice under a CU reservation)."""
     assert A.dtype == B.dtype == C.dtype and A.stride(-1) == 1 and B.stride(-1) == 1 and C.stride(-1) == 1
     M, N = C.shape
     K = A.shape[0] if a_kmajor else A.shape[1]
@@ -55,7 +56,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, op: str = "acc", a_k
         tp, ldt, tcols = _p(tneg), tneg.stride(0), tneg.shape[0]
     device_for(C).gemm(_DT[C.dtype], op, a_kmajor, M, N, K, _p(A), A.stride(0), _p(B), B.stride(0), _p(C), C.stride(0),
                        int(zero_cols[0]), int(zero_cols[1]), [int(r) for r in zero_rows], int(zero_row_height),
-                       tp, ldt, bool(latency), tcols)
+                       tp, ldt, bool(latency), tcols, bool(dense))
     return C
 
 

@@ -435,3 +435,24 @@ def test_block_inverse_live_grid_matches_full_grid(native, variant, m, dtype, p,
     assert torch.equal(inv_t[live], full[0][live])
     dead = np.flatnonzero(mine != 0)
     assert torch.equal(valid[dead], sentinel[2][dead]) and torch.equal(inv_t[dead], sentinel[0][dead])
+
+
+@pytest.mark.parametrize("M,N,K", [(2948, 2900, 520), (2950, 2902, 256), (4096, 2048, 1024)])
+@pytest.mark.parametrize("dense", [False, True])
+def test_gemm_glds_dense_build(native, M, N, K, dense):
+    """The 5-workgroups-per-CU build of the fp64 LDS-DMA trailing update (GemmExtra::dense, the
+    engine's choice under a CU reservation) against fp64 torch, with the zero-column / zero-row
+    extras and ragged edges, next to the default 4-per-CU build."""
+    A = _rand((M, K), torch.float64, 31)
+    B = _rand((K, N), torch.float64, 32)
+    C = _rand((M, N), torch.float64, 33)
+    z0, z1, zr, zh = 128, 384, [0, 1000, 2800], 128
+    Cin = C.clone()
+    Cin[:, z0:z1] = 0
+    for r in zr:
+        Cin[r:r + zh] = 0
+    ref = Cin + A @ B
+    Cd = C.cuda()
+    ops.gemm(A.t().contiguous().cuda(), B.cuda(), Cd, op="acc", a_kmajor=True, zero_cols=(z0, z1), zero_rows=zr,
+             zero_row_height=zh, dense=dense)
+    assert (Cd.cpu() - ref).abs().max().item() < 1e-12 * K
