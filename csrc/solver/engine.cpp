@@ -190,10 +190,11 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // p=8 emulation 0.191 vs 0.166 s -- concurrent GEMMs interleave their tiles, lose L2 locality and
   // crowd out the pivot path -- and were removed in round 3.)
   // COMM chunk-normalisation GEMMs (m x chunk width x m) on the small 64x32 latency tile: 4x the
-  // workgroups of the 128x64 tile.  Measured (profiles/small_n_sweep.md): N = 8192 30.2 -> 29.3 ms,
-  // but N = 16384 +1.1 % and N = 32768 +0.7 % (more COMM workgroups beside the trailing update), so
-  // only where the pivot chain dominates (padded order <= 8192).  GJ_COMM_SMALL_TILES overrides.
-  comm_small_tiles_ = L_.npad <= 8192;
+  // workgroups of the 128x64 tile.  Round 2 (profiles/small_n_sweep.md): N = 8192 30.2 -> 29.3 ms,
+  // N = 16384 +1.1 %, N = 32768 +0.7 %.  Round 4, with the look-ahead rows on SIDE the chunk pass
+  // is off the pivot chain at every size: N = 8192 25.80 / 25.74 (small) vs 25.66 / 25.56 ms,
+  // N = 16384 even (scripts/r4_cst.sh) -- off by default; GJ_COMM_SMALL_TILES=1 turns it on.
+  comm_small_tiles_ = false;
   // Look-ahead rows on SIDE, right behind the panel pieces, at every p (GJ_LA_SIDE=0 puts them on
   // COMM at p = 1, round 3's one-rank choice): with the host-free pivot chain, COMM's queue (the
   // previous panel's chunk pass, waiting for MAIN) is what held them back.  Round 4, same box,
