@@ -21,9 +21,9 @@ every collective of the solve is RCCL, issued by the native engine from C++.
 Failure handling: every host wait of the engine is bounded by ``--comm-timeout`` (default 90 s,
 below the driver's 600 s), so a hung peer turns into a non-zero exit on every rank, each naming
 its step, phase and the collective it sat in.  A wrong inverse is a failure too: after the timed
-loop the residual ||A A^-1 - I||_inf (the reference's check, main.cpp:490-507) is compared with
-``utils.metrics.residual_bound`` for the generator and size; non-finite or above the bound, the
-JSON line says ``"check": "residual_failed"`` and every rank exits 2.
+loop the residual ||A A^-1 - I||_inf (the reference's check, main.cpp:490-507) is normalised by
+||A|| ||A^-1|| eps and gated at 2n (``utils.metrics``, LAPACK's inverse test ratio); non-finite or
+above the gate, the JSON line says ``"check": "residual_failed"`` and every rank exits 2.
 
 ``--same-gpu`` (rehearsal on a one-GPU box): all ranks share device 0 and RCCL is told that every
 rank is its own host (``NCCL_HOSTID``), so it accepts the duplicate device and connects the ranks
@@ -213,13 +213,14 @@ def run_rank(args) -> int:
         sys.stdout.flush()
         os._exit(2)
 
+    comm_mode = {"one_comm": False, "hw_queues": None, "reason": ""}
     try:
         if not gpu:
             dev = C.host_device(args.host_threads)
-            if world > 1 and os.environ.get("GJ_TEST_HW_QUEUES"):  # the GPU path's agreement, rehearsed
-                from mpi_jordan_crazy_acceleration_amd.parallel.dist import agree_hw_queues
+            if world > 1:  # the GPU path's agreement, rehearsed (GJ_TEST_HW_QUEUES fakes a count)
+                from mpi_jordan_crazy_acceleration_amd.parallel.dist import agree_comm_mode
 
-                agree_hw_queues()
+                comm_mode = agree_comm_mode()
             if world > 1:
                 from mpi_jordan_crazy_acceleration_amd.parallel.dist import TorchDistComm
 
@@ -227,15 +228,15 @@ def run_rank(args) -> int:
             else:
                 comm = C.self_comm()
         elif world > 1 or args.force_rccl:
-            if world > 1:  # every rank fails together, before any RCCL communicator exists
-                from mpi_jordan_crazy_acceleration_amd.parallel.dist import agree_hw_queues
+            if world > 1:  # every rank takes the same communicator schedule, before any exists
+                from mpi_jordan_crazy_acceleration_amd.parallel.dist import agree_comm_mode
 
-                agree_hw_queues()
+                comm_mode = agree_comm_mode()
             ids = [[C.rccl_unique_id(), C.rccl_unique_id()] if rank == 0 else None]
             if world > 1:
                 dist.broadcast_object_list(ids, src=0)
             dev = C.hip_device(local)
-            comm = C.rccl_comm(ids[0], world, rank, local)
+            comm = C.rccl_comm(ids[0], world, rank, local, one_comm=comm_mode["one_comm"])
         else:
             dev = C.hip_device(local)
             comm = C.self_comm()
@@ -272,6 +273,15 @@ def run_rank(args) -> int:
             stats.append(step())
         barrier()
         t1 = time.perf_counter()
+        # p > 1: one extra UNTIMED solve with the per-phase device timers, so a multi-GPU record
+        # carries its own phase breakdown and host waits (the timed steps stay unprofiled)
+        prof = None
+        if world > 1 and not args.profile:
+            eng.set_profile(True)
+            prof = step()
+            eng.set_profile(False)
+            if prof["status"] != 0:
+                return fail(f"profiled solve failed with status {prof['status']}")
     except RuntimeError as e:
         return fail(e)
     st = stats[-1] if stats else {"status": 0, "offdiag_pivots": 0, "host_wait_ms": 0.0, "seconds": 0.0}
@@ -280,7 +290,9 @@ def run_rank(args) -> int:
         "ms": ms,
         "solve_s": [s["seconds"] for s in stats],
         "host_wait_ms": max([s["host_wait_ms"] for s in stats] or [0.0]),
-        "phases": stats[-1].get("phases") if stats else None,
+        "phases": (prof or (stats[-1] if stats else {})).get("phases"),
+        "profiled_solve_s": prof["seconds"] if prof else None,
+        "profiled_host_wait_ms": prof["host_wait_ms"] if prof else None,
         "policy": eng.policy,
         "rccl_transport": None,
     }
@@ -295,19 +307,27 @@ def run_rank(args) -> int:
         everyone = [mine]
     ms = max(e["ms"] for e in everyone)
     res = None
+    norm_a = norm_inv = None
     if not args.no_residual and st["status"] == 0:
         try:
+            norm_a = eng.input_norm_inf()
+            norm_inv = eng.result_norm_inf()
             res = eng.residual_generated(args.gen, args.seed)
         except RuntimeError as e:
             return fail(e)
     gflops = 2.0 * float(args.n) ** 3 / (ms / 1e3) / 1e9
-    from mpi_jordan_crazy_acceleration_amd.utils.metrics import residual_bound, residual_ok
+    from mpi_jordan_crazy_acceleration_amd.utils.metrics import (RHO_PER_N, residual_bound, residual_ok,
+                                                                  residual_ratio)
 
-    bound = residual_bound(args.gen, args.n, args.dtype)
+    bound = rho = None
     if args.no_residual:
         check = "skipped"
     else:
-        check = "residual_ok" if residual_ok(res, args.gen, args.n, args.dtype) else "residual_failed"
+        bound = residual_bound(args.n, norm_a or 0.0, norm_inv or 0.0, args.dtype)
+        bound = bound if bound == bound and bound != float("inf") else None  # strict JSON
+        rho = residual_ratio(res, norm_a or 0.0, norm_inv or 0.0, args.dtype)
+        check = "residual_ok" if residual_ok(res, args.n, norm_a or 0.0, norm_inv or 0.0, args.dtype) \
+            else "residual_failed"
     if rank == 0:
         pol = dict(mine["policy"])
         solve_all = [x for e in everyone for x in e["solve_s"]]
@@ -343,6 +363,7 @@ def run_rank(args) -> int:
             },
             "ranks": world,
             "comm": pol.pop("comm"),
+            "comm_mode": comm_mode,
             "bcast_tuning": pol.pop("bcast_tuning"),
             "policy": pol,
             "solve_seconds_max": round(max(solve_all or [0.0]), 4),
@@ -353,6 +374,12 @@ def run_rank(args) -> int:
             "rccl_transport": _merge_transports([e["rccl_transport"] for e in everyone]),
             "residual_inf": res,
             "residual_bound": bound,
+            # normalised residual ||A X - I|| / (||A|| ||X|| eps), gated at RHO_PER_N * n
+            "residual_ratio": (round(rho, 4) if rho is not None and rho != float("inf") else
+                               (None if rho is None else "inf")),
+            "residual_ratio_bound": RHO_PER_N * args.n,
+            "norm_a_inf": norm_a,
+            "norm_inv_inf": norm_inv,
             "check": check,
             "status": st["status"],
             "offdiag_pivots": st["offdiag_pivots"],
@@ -365,18 +392,25 @@ def run_rank(args) -> int:
                for p in pols):
             out["policy_per_rank"] = [{k: v for k, v in p.items() if k not in ("comm", "bcast_tuning")}
                                       for p in pols]
-        if args.profile:
+        if args.profile or prof is not None:
             phases = {}
             for e in everyone:
                 for name, v in (e["phases"] or {}).items():
                     phases[name] = max(phases.get(name, 0.0), round(v["ms"], 3))
             out["phases_ms_max"] = phases
+        if prof is not None:
+            out["profiled_solve"] = {
+                "timed": False,
+                "seconds_per_rank": [round(e["profiled_solve_s"], 4) for e in everyone],
+                "host_wait_ms_per_rank": [round(e["profiled_host_wait_ms"], 3) for e in everyone],
+            }
         print(json.dumps(out), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
     if check == "residual_failed":
-        print(f"bench.py: rank {rank}: residual {res} exceeds the bound {bound} for --gen {args.gen} "
-              f"N={args.n} {args.dtype}: wrong inverse", file=sys.stderr, flush=True)
+        print(f"bench.py: rank {rank}: residual {res} exceeds the bound {bound} (normalised {rho} > "
+              f"{RHO_PER_N} n) for --gen {args.gen} N={args.n} {args.dtype}: wrong inverse",
+              file=sys.stderr, flush=True)
         return 2
     return 0
 

@@ -14,6 +14,7 @@
 //   --gpus P             alias of --ranks for GPU runs
 //   --device gpu|cpu     execution backend (default: gpu when a HIP device exists)
 //   --comm auto|rccl|loopback|async   (async: stream-ordered virtual ranks; --jitter US)
+//   --one-comm           rccl: one communicator for the SIDE and COMM roles (also GJ_ONE_COMM=1)
 //   --dtype fp64|fp32
 //   --gen absdiff|hilbert|random|randshift|identity   generator when no file is given (reference: absdiff;
 //                        -DHILBERT -> --gen hilbert)
@@ -26,7 +27,7 @@
 //   --pivot block-min-inv-norm|partial   pivot rule (default: the reference's smallest ||inv||;
 //                        partial = block partial pivoting, one candidate inverse per rank and step)
 //   --pivot-growth G     partial pivoting: a candidate with ||inv||_inf * max|W| > G counts as
-//                        singular (default 1e8; 0 = off)
+//                        singular (default by dtype: 1e8 fp64, 8.4e4 fp32; 0 = off)
 //   --repeat R           time R solves, report the last (min also in --json)
 //   --out FILE           write the inverse (text, or .bin)
 //   --rhs ones|random|FILE  also solve A x = b (x = inv(A) b) and report ||A x - b||_inf
@@ -37,6 +38,8 @@
 //   --bcast auto|ring|direct  pivot-row broadcast algorithm at p > 2 (sets GJ_BCAST; auto = timed
 //                        against each other at startup, Comm::tune_bcast)
 //   --sync-debug         synchronise after every phase (race screening)
+//   --verify             consumption-point hashes of every broadcast buffer, compared across ranks
+//                        after the solve (also GJ_VERIFY=1; a mismatch fails with the step named)
 //   --race-check         run under the happens-before schedule checker (RaceCheckDevice): every
 //                        unordered conflicting access is printed to stderr and the exit code is 2
 //   --check-residual TOL exit 2 (after the normal output) when the residual is not finite or
@@ -113,6 +116,7 @@ int main(int argc, char* argv[]) {
     setenv("HIP_FORCE_DEV_KERNARG", "1", 0);
   }
   RunConfig cfg;
+  if (const char* e = std::getenv("GJ_ONE_COMM")) cfg.one_comm = std::atoi(e) != 0;
   std::vector<const char*> pos;
   bool json = false;
   std::string device = "auto", out_file, x_file;
@@ -131,6 +135,7 @@ int main(int argc, char* argv[]) {
       if (a == "-p" || a == "--ranks" || a == "--gpus") cfg.ranks = std::atoi(val(a.c_str()));
       else if (a == "--device") device = val("--device");
       else if (a == "--comm") cfg.comm = val("--comm");
+      else if (a == "--one-comm") cfg.one_comm = true;
       else if (a == "--jitter") cfg.jitter_us = std::atof(val("--jitter"));
       else if (a == "--dtype") {
         const std::string d = val("--dtype");
@@ -175,6 +180,7 @@ int main(int argc, char* argv[]) {
         setenv("GJ_BCAST", b.c_str(), 1);
       }
       else if (a == "--sync-debug") cfg.solve.sync_debug = true;
+      else if (a == "--verify") cfg.solve.verify = true;
       else if (a == "--race-check") cfg.race_check = true;
       else if (a == "--check-residual") check_tol = std::atof(val("--check-residual"));
       else if (a == "--profile") cfg.solve.profile = true;
@@ -230,6 +236,7 @@ int main(int argc, char* argv[]) {
       std::printf(rep.status == Status::Singular ? "singular matrix\n" : "not enough memory for block\n");
       if (json) json_report(cfg, rep);
       return 2;
+    case Status::VerifyFailed: std::fprintf(stderr, "gj: %s\n", rep.message.c_str()); return 2;
     default: std::printf("error: %s\n", rep.message.c_str()); return 2;
   }
   std::printf("A\n");

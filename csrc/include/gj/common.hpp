@@ -38,6 +38,7 @@ enum class Status : int {
   BadArgs = 5,
   CommError = 6,
   NoBlockMemory = 7,   // "not enough memory for block" (the elimination work space, main.cpp:428-436)
+  VerifyFailed = 8,    // GJ_VERIFY: a rank consumed a broadcast buffer whose bytes differ from the root's
 };
 
 class Error : public std::runtime_error {

@@ -21,7 +21,17 @@ class RcclComm : public Comm {
   static constexpr int kIdBytes = 128;
   static std::string unique_id();  // opaque bytes (kIdBytes)
   // ids: one unique id per communicator (2); every rank passes the same ids.
-  RcclComm(const std::vector<std::string>& ids, int nranks, int rank, int device);
+  // one_comm (every rank passes the same value): the SIDE and COMM roles share ONE communicator
+  // (ids[0]; ids[1] unused).  RCCL runs a communicator's kernels one after another in issue order,
+  // and every rank issues its collectives in the same program order with every cross-stream edge
+  // an event that points back in that order, so no cross-rank wait cycle can form however the
+  // streams share hardware queues: the schedule for processes with fewer than kMinHwQueues
+  // hardware queues (the SIDE collectives then queue behind the chunk broadcasts issued before
+  // them: slower, never stuck).  With two communicators each needs its own queue (README
+  // "Progress of the two communicators"); that condition is the launcher's to check, since only
+  // it knows the count HIP really initialised with (parallel/dist.py agree_comm_mode).
+  RcclComm(const std::vector<std::string>& ids, int nranks, int rank, int device, bool one_comm = false);
+  bool one_comm() const { return one_comm_; }
   ~RcclComm() override;
   int size() const override { return n_; }
   int rank() const override { return r_; }
@@ -45,6 +55,7 @@ class RcclComm : public Comm {
  private:
   void* comm_for(int s) const;
   int n_ = 1, r_ = 0, device_ = 0;
+  bool one_comm_ = false;
   void* comms_[2] = {nullptr, nullptr};  // ncclComm_t
   void* dbuf_ = nullptr;                 // small device scratch for host helpers
   size_t dbuf_sz_ = 0;

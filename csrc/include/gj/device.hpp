@@ -279,6 +279,14 @@ class Device {
   virtual void permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx,
                               int64_t nblk, int64_t m, int64_t Nr, const int32_t* dst_blk,
                               const int32_t* colsrc, int s) = 0;
+  // Consumption-point verification (GJ_VERIFY, Engine): a position-dependent 64-bit hash of the
+  // bytes [r*ld_bytes, r*ld_bytes + width_bytes) of rows r < rows at `base` (width a multiple of 4),
+  // as kHashParts partial sums that add (mod 2^64) to the hash of those bytes (gen.hpp hash_term) --
+  // enqueued on the stream that consumes the buffer, right before its consumer, so it sees what the
+  // consumer saw.
+  static constexpr int kHashParts = 64;
+  virtual void hash_rows(const void* base, int64_t ld_bytes, int64_t width_bytes, int64_t rows,
+                         uint64_t* parts, int s) = 0;
   // out[0] = max over local real rows of sum_{j<n} |X[r][j]|  (reference norm(), main.cpp:643-667).
   virtual void row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out,
                            int s) = 0;

@@ -58,10 +58,25 @@ struct SolveOptions {
   PivotRule pivot = PivotRule::MinInvNorm;
   // PivotRule::Partial: a rank's candidate whose growth estimate ||inv(W)||_inf * max|W| exceeds
   // this is treated as singular (another rank's, or the full MinInvNorm search, takes the step), so
-  // partial pivoting cannot silently accept a near-singular block.  <= 0: no guard.
-  double pivot_growth = 1e8;
+  // partial pivoting cannot silently accept a near-singular block.  0: no guard; < 0 (default): by
+  // dtype, min(1e8, 0.01 / eps) -- 1e8 for fp64, 8.4e4 for fp32 (a dtype-blind 1e8
+  // accepted fp32 blocks whose inverse has no correct digit; the estimate can understate
+  // cond_inf by up to m, hence the margin below 1 / eps).
+  double pivot_growth = -1;
+  double pivot_growth_bound() const {
+    if (pivot_growth >= 0) return pivot_growth;
+    const double e = dtype == DType::F64 ? 2.220446049250313e-16 : 1.1920928955078125e-07;
+    return std::min(1e8, 0.01 / e);
+  }
   bool sync_debug = false;  // synchronise every stream after every phase (race screening)
   bool profile = false;     // per-phase device timers (HIP events) + roctx ranges
+  // Consumption-point verification (also GJ_VERIFY=1): every broadcast buffer is hashed on the
+  // stream that consumes it, right before its consumer (MAIN: each Rb chunk segment; SIDE: each
+  // panel piece, look-ahead row segment, gathered pivot records and the pivot sequence; COMM: the
+  // last piece).  After the solve the hashes are all-gathered and compared with the root's; the
+  // first mismatch (in step order) fails the solve on every rank with Status::VerifyFailed, naming
+  // step, phase, buffer, root, the differing receivers and the consuming stream.
+  bool verify = false;
   double comm_timeout_s = 600;  // a host wait on a pivot longer than this is a peer failure
   int reserve_cus = -1;     // CUs kept free of the trailing update for the pivot path (-1 = auto)
 };
@@ -133,6 +148,9 @@ class Engine {
 
   // ---- solve (collective) ----
   SolveStats solve();
+  // Per-phase device timers for the following solves (SolveOptions::profile), switchable between
+  // solves: bench.py times its steps unprofiled, then profiles one extra untimed solve.
+  void set_profile(bool on) { opt_.profile = on; }
 
   // ---- output ----
   void* result_panel() { return out_; }  // local rows of inv(A), padded, ld npad
@@ -156,8 +174,17 @@ class Engine {
   // Collective; b and x are full n-vectors on every rank.
   RhsResult solve_rhs(const double* b, double* x, const GenSpec* gen, const double* host_rows, int64_t ld,
                       int max_refine, double tol);
+  // The same with this rank's real rows of A as an fp64 DEVICE array (ld >= n elements), e.g. a
+  // torch CUDA tensor: copied device-to-device, never through the host.
+  RhsResult solve_rhs_device(const double* b, double* x, const void* dev_rows_f64, int64_t ld, int max_refine,
+                             double tol);
   // Precision of the last residual: true = fp64 (always for fp64 solves; fp32 solves when it fits).
   bool residual_fp64() const { return last_residual_fp64_; }
+  // ||A||_inf of the last solve's input (the reference's norm, taken at solve start) and
+  // ||inv(A)||_inf of its result (collective): the scale of the normalised residual
+  // ||A inv(A) - I|| / (||A|| ||inv(A)|| eps) that utils/metrics.py gates on.
+  double input_norm_inf() const { return norm_a_; }
+  double result_norm_inf();
 
   int64_t real_local_rows() const;
   int depth() const { return d_; }  // elimination steps per panel (after the auto choice)
@@ -172,6 +199,7 @@ class Engine {
     bool dense_gemm = false;      // trailing update at 5 workgroups per CU
     bool la_side = true;          // look-ahead rows on SIDE (else COMM)
     std::string pivot;            // "block-min-inv-norm" | "partial"
+    std::string fault_injection;  // active GJ_TEST_* knobs ("" in every normal run)
   };
   Policy policy() const;
   const std::string& bcast_algo() const { return bcast_algo_; }  // "ring" | "direct"
@@ -210,6 +238,17 @@ class Engine {
   void big_update(int64_t u);
   void finalize(const std::vector<int32_t>& seq);
   SolveStats solve_steps();
+  RhsResult solve_rhs_impl(const double* b, double* x, const GenSpec* gen, const double* host_rows,
+                           const void* dev_rows, int64_t ld, int max_refine, double tol);
+  // GJ_VERIFY (SolveOptions::verify): hash slots of a panel, (d*C + 3d + 1) of them:
+  //   [chunk c][step j] Rb segment at MAIN's chunk update | pp[j] panel piece at its first consumer
+  //   | la[j] look-ahead row segment at the look-ahead update | recs[j] gathered pivot records |
+  //   seq (the panel's pivot sequence, after its last step)
+  enum VKind { V_RB = 0, V_PP, V_LA, V_RECS, V_SEQ };
+  int vslot(VKind k, int64_t j, int64_t c = 0) const;
+  int vslots() const { return (int)(d_ * (int64_t)cb0_.size() + 3 * d_ + 1); }
+  void vhash(int64_t v, int slot, const void* base, int64_t ld_bytes, int64_t width_bytes, int64_t rows, int s);
+  void verify_hashes(const SolveStats& st);
   double residual_common(const void* A, bool wide);
   double residual_streamed(const void* A, bool wide);
   bool residual_wide();
@@ -291,6 +330,7 @@ class Engine {
   PivotRec* recs_ = nullptr;
   PivotResult* piv_dev_ = nullptr;
   double* dscratch_ = nullptr;
+  uint64_t* vparts_ = nullptr;  // GJ_VERIFY: npanels x vslots x Device::kHashParts partial hashes
   int32_t* iscratch_ = nullptr;
   // pinned host
   PivotResult* piv_host_ = nullptr;
@@ -320,6 +360,7 @@ class Engine {
   // where the solve is (named by communication-failure messages)
   int64_t cur_step_ = -1;
   const char* cur_phase_ = "setup";
+  std::string fault_injection_;  // active GJ_TEST_* knobs (announced, reported in policy())
   int64_t hang_step_ = -1;  // GJ_TEST_HANG (fault injection)
   int64_t corrupt_step_ = -1;  // GJ_TEST_CORRUPT (a wrong inverse on purpose)
   // GJ_TEST_DROP_WAIT=<name>[,<name>]: leave out one ordering edge of the schedule (a planted

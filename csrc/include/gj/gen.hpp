@@ -19,6 +19,12 @@ GJ_HD inline uint64_t splitmix64(uint64_t x) {
   return x ^ (x >> 31);
 }
 
+// Term of 32-bit word `w` at word index `idx` of a hashed buffer (Device::hash_rows): the hash is
+// the wrapping sum of the terms, so it is independent of the order the words are visited in.
+GJ_HD inline uint64_t hash_term(uint32_t w, uint64_t idx) {
+  return splitmix64(((uint64_t)w << 32) ^ (idx * 0xD1B54A32D192ED03ull) ^ 0x5851F42D4C957F2Dull);
+}
+
 // Element (i, j) of the padded matrix A' = diag(A, I) (i, j < npad).
 GJ_HD inline double gen_value(int kind, uint64_t seed, int64_t n, int64_t i, int64_t j) {
   if (i >= n || j >= n) return (i == j) ? 1.0 : 0.0;

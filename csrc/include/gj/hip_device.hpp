@@ -94,6 +94,8 @@ class HipDevice : public Device {
                       int s) override;
   void row_abs_max_minus_i(DType dt, const void* X, int64_t ldx, const Layout& L, double* out,
                            int s) override;
+  void hash_rows(const void* base, int64_t ld_bytes, int64_t width_bytes, int64_t rows, uint64_t* parts,
+                 int s) override;
   void row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out,
                    int s) override;
   void residual(DType dt, const void* A, const void* Full, const Layout& L, double* out,

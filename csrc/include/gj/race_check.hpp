@@ -231,6 +231,8 @@ class RaceCheckDevice : public Device {
   void gemm_batch(DType dt, const GemmDesc* d, int n, int s) override;
   void permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx, int64_t nblk, int64_t m,
                       int64_t Nr, const int32_t* dst_blk, const int32_t* colsrc, int s) override;
+  void hash_rows(const void* base, int64_t ld_bytes, int64_t width_bytes, int64_t rows, uint64_t* parts,
+                 int s) override;
   void row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out, int s) override;
   void row_abs_max_minus_i(DType dt, const void* X, int64_t ldx, const Layout& L, double* out, int s) override;
   void residual(DType dt, const void* A, const void* Full, const Layout& L, double* out, int s) override;

@@ -17,6 +17,7 @@ struct RunConfig {
   int ranks = 1;
   bool gpu = true;
   std::string comm = "auto";        // auto | rccl | loopback | async (stream-ordered virtual ranks)
+  bool one_comm = false;            // rccl: SIDE and COMM share one communicator (RcclComm, GJ_ONE_COMM)
   double jitter_us = 0.0;           // async: random per-rank arrival delay (tests)
   int first_device = 0;
   GenSpec gen;

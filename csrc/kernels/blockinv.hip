@@ -16,6 +16,8 @@
 // Outputs: the inverse (transposed, ready to be the K-major GEMM operand H^T), ||inv||_inf, validity.
 #include <hip/hip_runtime.h>
 
+#include <stdexcept>
+
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -95,7 +97,7 @@ __global__ __launch_bounds__(NTH) void block_inverse_kernel(const T* __restrict_
   __shared__ int kinv[MP];
   __shared__ int pos[MP];     // current position of every row under the reference's swaps
   __shared__ int posrow[MP];  // row at every position
-  __shared__ double red[MP];
+  __shared__ double red[NTH / 64][MP];  // per-wave partial row abs-sums (fixed-order reduction)
   __shared__ double wmax[NTH / 64];
 
   T w[RI][CJ];
@@ -110,7 +112,6 @@ __global__ __launch_bounds__(NTH) void block_inverse_kernel(const T* __restrict_
     }
   }
   for (int i = tid; i < MP; i += NTH) {
-    red[i] = 0.0;
     pos[i] = i;
     posrow[i] = i;
   }
@@ -237,7 +238,12 @@ __global__ __launch_bounds__(NTH) void block_inverse_kernel(const T* __restrict_
 
   if (piv_out)  // test probe: the pivot row of every column
     for (int c = tid; c < m; c += NTH) piv_out[(int64_t)b * m + c] = prow[c];
-  // ||inv||_inf = max row abs-sum of the swept block (row/column permutations do not change it)
+  // ||inv||_inf = max row abs-sum of the swept block (row/column permutations do not change it).
+  // Summed in a fixed order (the reference's block_norm is a sequential sum, main.cpp:669-683), so
+  // the score -- and with it the pivot sequence -- is the same bits on every run: the two half-waves
+  // of a wave (thread rows tr = 2w, 2w + 1) meet by one commutative exchange, then every row adds
+  // its per-wave partials in wave order.
+  const int wv = tid >> 6;
 #pragma unroll
   for (int qi = 0; qi < RI; ++qi) {
     const int i = tc + 32 * qi;
@@ -247,11 +253,17 @@ __global__ __launch_bounds__(NTH) void block_inverse_kernel(const T* __restrict_
       const int j = tr + TR * cj;
       if (j < m) s += fabs((double)w[qi][cj]);
     }
-    if (i < m) atomicAdd(&red[i], s);
+    s += __shfl_xor(s, 32, 64);
+    if (i < m && lane < 32) red[wv][i] = s;
   }
   __syncthreads();
   double mx = 0.0;
-  for (int i = tid; i < m; i += NTH) mx = fmax(mx, red[i]);
+  for (int i = tid; i < m; i += NTH) {
+    double rs = 0.0;
+#pragma unroll
+    for (int q = 0; q < NTH / 64; ++q) rs += red[q][i];
+    mx = fmax(mx, rs);
+  }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off, 64));
   if (lane == 0) wmax[tid >> 6] = mx;
@@ -739,10 +751,18 @@ static bool launch_blocked(const void* Lt, int64_t ldl, void* inv_t, double* sco
 // co-resident L2-image kernel (fp64 32 < m <= 128; GJ_BI_VARIANT=co), 6 = the per-step global
 // sweep for m > 256 instead of the panel-blocked kernel (reference timing)
 static int g_bi_variant = -1;
+int block_inverse_variant_id(const char* name) {
+  const std::string v(name);
+  if (v == "panel") return 0;
+  if (v == "sweep") return 1;
+  if (v == "co") return 5;
+  if (v == "generic") return 6;
+  throw std::invalid_argument("unknown block-inverse variant '" + v + "' (panel | sweep | co | generic)");
+}
 static int bi_variant() {
   if (g_bi_variant < 0) {
     const char* e = getenv("GJ_BI_VARIANT");
-    g_bi_variant = (e && std::string(e) == "co") ? 5 : 0;
+    g_bi_variant = (e && *e) ? block_inverse_variant_id(e) : 0;  // a typo throws
   }
   return g_bi_variant;
 }

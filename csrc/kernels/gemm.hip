@@ -31,6 +31,8 @@
 // with out-of-range offsets instead of branches (see kOOB).  Tiles are mapped XCD-aware (xcd_remap).
 #include <hip/hip_runtime.h>
 
+#include <stdexcept>
+
 #include <cstdint>
 #include <cstdlib>
 #include <string>
@@ -889,7 +891,7 @@ static int g_variant = -1;
 static int gemm_variant() {
   if (g_variant < 0) {
     const char* e = getenv("GJ_GEMM_VARIANT");
-    g_variant = e ? gemm_variant_id(e) : kAutoVariant;
+    g_variant = (e && *e) ? gemm_variant_id(e) : kAutoVariant;  // a typo throws: never a silent default
   }
   return g_variant;
 }
@@ -898,7 +900,7 @@ int gemm_variant_id(const char* name) {
   static const char* names[] = {"big", "narrow", "", "", "", "", "squarepf", "", "", "bigpf", "auto", "glds"};
   for (int i = 0; i < (int)(sizeof(names) / sizeof(names[0])); ++i)
     if (*names[i] && s == names[i]) return i;
-  return kAutoVariant;
+  throw std::invalid_argument("unknown GEMM variant '" + s + "' (big | narrow | squarepf | bigpf | glds | auto)");
 }
 void set_gemm_variant(int v) { g_variant = v; }
 

@@ -18,10 +18,11 @@ void gemm(DType dt, int op /*0 acc, 1 store*/, int a_kmajor, int64_t M, int64_t 
 // n independent small K-major GEMMs, one launch per 4 (small tiles; Store = C never read)
 void gemm_batch(DType dt, const GemmDesc* d, int n, hipStream_t s);
 int residual_nparts(int64_t N);
-int gemm_variant_id(const char* name);  // big | narrow | squarepf | bigpf | glds | auto
+int gemm_variant_id(const char* name);  // big | narrow | squarepf | bigpf | glds | auto; else throws
 void set_gemm_variant(int v);
 void set_block_inverse_variant(int v);  // 0 = default families, 1 = register sweep, 5 = co-resident, 6 = generic
 int block_inverse_variant();
+int block_inverse_variant_id(const char* name);  // panel | sweep | co | generic; else throws
 const char* block_inverse_kernel_name(DType dt, int64_t m, int variant);
 void residual_partial(DType dt, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                       const void* B, int64_t ldb, int64_t n_real, int64_t blk_m, int64_t p,
@@ -95,6 +96,9 @@ void h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, hipStrea
 void permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx, int64_t nblk,
                     int64_t m, int64_t Nr, const int32_t* dst_blk, const int32_t* colsrc,
                     hipStream_t s);
+// Device::hash_rows: nparts workgroups, parts[g] = workgroup g's partial hash
+void hash_rows(const void* base, int64_t ld_bytes, int64_t width_bytes, int64_t rows, uint64_t* parts,
+               int nparts, hipStream_t s);
 // minus_identity: sum_j |X[r][j] - delta(global(r), j)| (the streamed residual's row sums)
 void row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out, hipStream_t s,
                  bool minus_identity = false);

@@ -504,6 +504,34 @@ void permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx
                        static_cast<const float*>(X), ldx, (int)m, ncols, dst_blk, colsrc);
 }
 
+// ---------------------------------------------------------------- verification hash
+// parts[g] = sum (mod 2^64) of hash_term over the words workgroup g visits (grid-stride); every
+// workgroup writes its own part with one vector store (no atomics), the host adds the parts.
+__global__ __launch_bounds__(256) void hash_rows_kernel(const uint8_t* base, int64_t ld_bytes, int64_t wwords,
+                                                        int64_t rows, uint64_t* parts) {
+  const int64_t total = wwords * rows;
+  uint64_t h = 0;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t r = e / wwords, w = e - r * wwords;
+    const uint32_t v = *reinterpret_cast<const uint32_t*>(base + r * ld_bytes + 4 * w);
+    h += hash_term(v, (uint64_t)e);
+  }
+  __shared__ uint64_t sh[256];
+  sh[threadIdx.x] = h;
+  __syncthreads();
+  for (int o = 128; o >= 1; o >>= 1) {
+    if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) parts[blockIdx.x] = sh[0];
+}
+
+void hash_rows(const void* base, int64_t ld_bytes, int64_t width_bytes, int64_t rows, uint64_t* parts,
+               int nparts, hipStream_t s) {
+  hipLaunchKernelGGL(hash_rows_kernel, dim3((unsigned)nparts), dim3(256), 0, s, static_cast<const uint8_t*>(base),
+                     ld_bytes, width_bytes / 4, rows, parts);
+}
+
 // ---------------------------------------------------------------- norms
 template <typename T>
 __global__ __launch_bounds__(256) void row_abs_kernel(const T* X, int64_t ldx, int64_t n, int64_t m,

@@ -57,6 +57,7 @@ __device__ inline void pivot_finish(PivotRec best, int32_t p, int32_t t, int32_t
     r.score = best.score;
     pivot_commit(t, best.phys, pos, phys_at, used, seq);
   } else {
+    seq[t] = -1;  // the step's owner-predicated launches (enqueued ahead) stay no-ops on every rank
     r.found = 0;
     r.phys = -1;
     r.owner = -1;

@@ -169,11 +169,7 @@ PYBIND11_MODULE(_C, mod) {
   });
   mod.def("rccl_unique_id", [] { return py::bytes(RcclComm::unique_id()); });
   mod.def("set_block_inverse_variant", [](const std::string& v) {
-    if (v == "panel") kern::set_block_inverse_variant(0);
-    else if (v == "sweep") kern::set_block_inverse_variant(1);
-    else if (v == "co") kern::set_block_inverse_variant(5);
-    else if (v == "generic") kern::set_block_inverse_variant(6);
-    else throw std::invalid_argument("block inverse variant: panel | sweep | co | generic");
+    kern::set_block_inverse_variant(kern::block_inverse_variant_id(v.c_str()));
   });
   mod.def("set_block_inverse_probe", [](uintptr_t p) { kern::set_block_inverse_probe(reinterpret_cast<int32_t*>(p)); },
           "test probe: device int32 buffer (nblk x m) receiving each candidate's pivot row per column; 0 = off");
@@ -333,12 +329,15 @@ PYBIND11_MODULE(_C, mod) {
            py::arg("device"), py::arg("bytes"));
   mod.def("self_comm", [] { return std::shared_ptr<Comm>(new SelfComm()); });
   mod.def("rccl_comm",
-          [](std::vector<py::bytes> ids, int nranks, int rank, int device) {
+          [](std::vector<py::bytes> ids, int nranks, int rank, int device, bool one_comm) {
             std::vector<std::string> s;
             for (auto& b : ids) s.push_back(std::string(b));
             py::gil_scoped_release rel;
-            return std::shared_ptr<Comm>(new RcclComm(s, nranks, rank, device));
-          });
+            return std::shared_ptr<Comm>(new RcclComm(s, nranks, rank, device, one_comm));
+          },
+          py::arg("ids"), py::arg("nranks"), py::arg("rank"), py::arg("device"), py::arg("one_comm") = false,
+          "one_comm: the SIDE and COMM roles share one communicator (every rank must pass the same value; "
+          "parallel.dist.agree_comm_mode decides it)");
   mod.def("shadow_comm", [](int p, double bw_gbs, double lat_us, int channels, int lds_kib, bool direct) {
             CostModel cm;
             cm.bw_gbs = bw_gbs;
@@ -425,7 +424,7 @@ PYBIND11_MODULE(_C, mod) {
            py::arg("device"), py::arg("comm"), py::arg("n"), py::arg("m"), py::arg("dtype") = "fp64",
            py::arg("chunk_cols") = 0, py::arg("eps") = kDefaultEps, py::arg("sync_debug") = false,
            py::arg("depth") = 0, py::arg("profile") = false, py::arg("comm_timeout_s") = 600.0,
-           py::arg("pivot") = "block-min-inv-norm", py::arg("pivot_growth") = 1e8)
+           py::arg("pivot") = "block-min-inv-norm", py::arg("pivot_growth") = -1.0)
       .def_property_readonly("layout",
                              [](PyEngine& e) {
                                const Layout& L = e.eng->layout();
@@ -450,6 +449,7 @@ PYBIND11_MODULE(_C, mod) {
                                d["dense_gemm"] = pl.dense_gemm;
                                d["look_ahead_rows"] = pl.la_side ? "SIDE" : "COMM";
                                d["pivot"] = pl.pivot;
+                               if (!pl.fault_injection.empty()) d["fault_injection"] = pl.fault_injection;
                                d["bcast"] = e.eng->bcast_algo();
                                d["bcast_tuning"] = e.comm->bcast_report();
                                d["comm"] = e.comm->describe();
@@ -487,12 +487,47 @@ PYBIND11_MODULE(_C, mod) {
              e.eng->download_rows_device(reinterpret_cast<void*>(ptr), ld);
            },
            py::arg("ptr"), py::arg("ld"))
+      .def("solve_rhs_device",
+           [](PyEngine& e, py::array_t<double, py::array::c_style | py::array::forcecast> b, uintptr_t rows,
+              int64_t ld, int max_refine, double tol) {
+             const int64_t n = e.eng->layout().n;
+             if (b.ndim() != 1 || b.shape(0) != n) throw std::invalid_argument("b must be an n-vector");
+             if (ld < n) throw std::invalid_argument("ld < n");
+             if (max_refine < 0) max_refine = e.eng->options().dtype == DType::F64 ? 2 : 10;
+             py::array_t<double> x(n);
+             RhsResult rr;
+             {
+               py::gil_scoped_release rel;
+               rr = e.eng->solve_rhs_device(b.data(), x.mutable_data(), reinterpret_cast<const void*>(rows), ld,
+                                            max_refine, tol);
+             }
+             py::dict info;
+             info["residual"] = rr.residual;
+             info["backward_error"] = rr.backward_error;
+             info["history"] = rr.history;
+             info["steps"] = rr.steps;
+             info["converged"] = rr.converged;
+             return py::make_tuple(x, info);
+           },
+           py::arg("b"), py::arg("rows_f64"), py::arg("ld"), py::arg("max_refine") = -1, py::arg("tol") = 1e-15,
+           "A x = b after solve(): x = inv(A) b by the native GEMV, refined in fp64 against this rank's rows "
+           "of A given as an fp64 device array (Engine::solve_rhs_device); returns (x, info)")
       .def("input_panel_ptr", [](PyEngine& e) { return (uintptr_t)e.eng->input_panel(); })
       .def("result_panel_ptr", [](PyEngine& e) { return (uintptr_t)e.eng->result_panel(); })
       .def("norm_inf", [](PyEngine& e) {
         py::gil_scoped_release rel;
         return e.eng->norm_inf();
       })
+      .def("input_norm_inf", [](PyEngine& e) { return e.eng->input_norm_inf(); },
+           "||A||_inf of the last solve's input")
+      .def("result_norm_inf",
+           [](PyEngine& e) {
+             py::gil_scoped_release rel;
+             return e.eng->result_norm_inf();
+           },
+           "||inv(A)||_inf of the last solve's result (collective)")
+      .def("set_profile", [](PyEngine& e, bool on) { e.eng->set_profile(on); },
+           "per-phase device timers for the following solves (between solves only)")
       .def("solve", [](PyEngine& e) {
         SolveStats st;
         {
@@ -582,6 +617,8 @@ PYBIND11_MODULE(_C, mod) {
     if (d.contains("chunk_cols")) c.solve.chunk_cols = d["chunk_cols"].cast<int64_t>();
     if (d.contains("eps")) c.solve.eps = d["eps"].cast<double>();
     if (d.contains("sync_debug")) c.solve.sync_debug = d["sync_debug"].cast<bool>();
+    if (d.contains("verify")) c.solve.verify = d["verify"].cast<bool>();
+    if (d.contains("one_comm")) c.one_comm = d["one_comm"].cast<bool>();
     if (d.contains("depth")) c.solve.depth = d["depth"].cast<int>();
     if (d.contains("pivot")) c.solve.pivot = parse_pivot(d["pivot"].cast<std::string>());
     if (d.contains("pivot_growth")) c.solve.pivot_growth = d["pivot_growth"].cast<double>();

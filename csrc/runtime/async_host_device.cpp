@@ -321,6 +321,11 @@ void AsyncHostDevice::row_abs_max_minus_i(DType dt, const void* X, int64_t ldx, 
                                           int s) {
   enqueue(s, [=] { inner_.row_abs_max_minus_i(dt, X, ldx, L, out, s); });
 }
+void AsyncHostDevice::hash_rows(const void* base, int64_t ld_bytes, int64_t width_bytes, int64_t rows,
+                                uint64_t* parts, int s) {
+  enqueue(s, [=] { inner_.hash_rows(base, ld_bytes, width_bytes, rows, parts, s); });
+}
+
 void AsyncHostDevice::row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out,
                                   int s) {
   enqueue(s, [=] { inner_.row_abs_max(dt, X, ldx, L, out, s); });

@@ -341,6 +341,11 @@ void HipDevice::row_abs_max_minus_i(DType dt, const void* X, int64_t ldx, const 
   kern::row_abs_max(dt, X, ldx, L, out, hs(streams_[s]), true);
   check_launch();
 }
+void HipDevice::hash_rows(const void* base, int64_t ld_bytes, int64_t width_bytes, int64_t rows, uint64_t* parts,
+                          int s) {
+  kern::hash_rows(base, ld_bytes, width_bytes, rows, parts, kHashParts, hs(streams_[s]));
+}
+
 void HipDevice::row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out,
                             int s) {
   kern::row_abs_max(dt, X, ldx, L, out, hs(streams_[s]));

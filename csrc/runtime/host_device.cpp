@@ -342,6 +342,7 @@ void HostDevice::pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_
     r.score = best.score;
     pivot_commit(t, best.phys, pos, phys_at, used, seq);
   } else {
+    seq[t] = -1;  // as the GPU kernel: the step's owner-predicated launches stay no-ops
     r.found = 0;
     r.phys = -1;
     r.owner = -1;
@@ -465,6 +466,20 @@ void HostDevice::row_abs_max_minus_i(DType dt, const void* X, int64_t ldx, const
     mx = std::max(mx, s);
   }
   out[0] = mx;
+}
+
+void HostDevice::hash_rows(const void* base, int64_t ld_bytes, int64_t width_bytes, int64_t rows,
+                           uint64_t* parts, int) {
+  const int64_t ww = width_bytes / 4;
+  uint64_t h = 0;
+  for (int64_t r = 0; r < rows; ++r)
+    for (int64_t w = 0; w < ww; ++w) {
+      uint32_t v;
+      std::memcpy(&v, static_cast<const char*>(base) + r * ld_bytes + 4 * w, 4);
+      h += hash_term(v, (uint64_t)(r * ww + w));
+    }
+  parts[0] = h;
+  for (int g = 1; g < kHashParts; ++g) parts[g] = 0;
 }
 
 void HostDevice::row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out,

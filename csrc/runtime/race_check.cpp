@@ -686,6 +686,13 @@ void RaceCheckDevice::permute_blocks(DType dt, void* dst, int64_t ldd, const voi
          R(span(colsrc, 4 * Nr), "colsrc"), W(rect(dst, ldd, Nr * m, nblk * m, es), "dst")});
   inner_->permute_blocks(dt, dst, ldd, X, ldx, nblk, m, Nr, dst_blk, colsrc, s);
 }
+void RaceCheckDevice::hash_rows(const void* base, int64_t ld_bytes, int64_t width_bytes, int64_t rows,
+                                uint64_t* parts, int s) {
+  check(s, "hash_rows", {R(rect(base, ld_bytes, width_bytes, rows, 1), "buffer"),
+                         W(span(parts, sizeof(uint64_t) * kHashParts), "parts")});
+  inner_->hash_rows(base, ld_bytes, width_bytes, rows, parts, s);
+}
+
 void RaceCheckDevice::row_abs_max(DType dt, const void* X, int64_t ldx, const Layout& L, double* out, int s) {
   check(s, "row_abs_max", {R(rect(X, ldx, L.n, L.rows, (int64_t)dtype_size(dt)), "X"), W(span(out, 8), "out")});
   inner_->row_abs_max(dt, X, ldx, L, out, s);

@@ -37,23 +37,23 @@ std::string RcclComm::unique_id() {
   return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
 }
 
-RcclComm::RcclComm(const std::vector<std::string>& ids, int nranks, int rank, int device)
-    : n_(nranks), r_(rank), device_(device) {
+RcclComm::RcclComm(const std::vector<std::string>& ids, int nranks, int rank, int device, bool one_comm)
+    : n_(nranks), r_(rank), device_(device), one_comm_(one_comm) {
   GJ_REQUIRE(ids.size() == 2, "RcclComm needs two unique ids");
-  {
-    // The SIDE and COMM communicators must not share an in-order hardware queue (README "Progress
-    // of the two communicators").  Every rank reads the same environment (the CLI sets it before
-    // the first HIP call; the Python launchers agree on the value first, parallel/dist.py
-    // agree_hw_queues), so this refusal happens on every rank, before any communicator exists.
+  if (nranks > 1 && !one_comm_) {
+    // Two concurrently active communicators need their own hardware queues (README "Progress of
+    // the two communicators").  The launchers agree on the count HIP really runs with and pick
+    // the one-communicator schedule below 16 (parallel/dist.py agree_comm_mode, cli/main.cpp);
+    // here only the environment is visible, so an embedder that constructs this directly is warned.
     const char* q = std::getenv("GPU_MAX_HW_QUEUES");
-    if (nranks > 1 && (!q || std::atoi(q) < kMinHwQueues))
-      throw Error(Status::CommError, std::string("GPU_MAX_HW_QUEUES=") + (q ? q : "unset") + " < " +
-                                         std::to_string(kMinHwQueues) +
-                                         ": the SIDE and COMM communicators could share a hardware queue "
-                                         "(set it before the first HIP call, see runtime_env.py)");
+    if (!q || std::atoi(q) < kMinHwQueues)
+      std::fprintf(stderr,
+                   "gj: warning: two RCCL communicators with GPU_MAX_HW_QUEUES=%s < %d: they may share a "
+                   "hardware queue; pass one_comm (GJ_ONE_COMM=1) unless HIP was initialised with more\n",
+                   q ? q : "unset", kMinHwQueues);
   }
   (void)hipSetDevice(device_);
-  for (int c = 0; c < 2; ++c) {
+  for (int c = 0; c < (one_comm_ ? 1 : 2); ++c) {
     GJ_REQUIRE(ids[c].size() == sizeof(ncclUniqueId), "bad unique id size");
     ncclUniqueId id;
     std::memcpy(&id, ids[c].data(), sizeof(id));
@@ -75,12 +75,13 @@ RcclComm::~RcclComm() {
 std::string RcclComm::describe() const {
   int v = 0;
   ncclGetVersion(&v);
-  return "rccl(v" + std::to_string(v) + ", " + std::to_string(n_) + " ranks)";
+  return "rccl(v" + std::to_string(v) + ", " + std::to_string(n_) + " ranks" +
+         (one_comm_ ? ", one communicator)" : ")");
 }
 
 void* RcclComm::comm_for(int s) const {
   GJ_REQUIRE(s == S_SIDE || s == S_COMM, "RCCL collectives are only issued on SIDE/COMM streams");
-  return comms_[s == S_SIDE ? 0 : 1];
+  return comms_[(s == S_SIDE || one_comm_) ? 0 : 1];
 }
 
 static inline hipStream_t st(Device& dev, int s) { return static_cast<hipStream_t>(dev.native_stream(s)); }

@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
@@ -86,6 +87,7 @@ int64_t injected_step(const char* var, int rank) {
 Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions& opt)
     : dev_(dev), comm_(comm), opt_(opt) {
   GJ_REQUIRE(n > 0 && m > 0, "n and m must be positive");
+  if (const char* e = std::getenv("GJ_VERIFY")) opt_.verify = opt_.verify || std::atoi(e) != 0;
   L_ = Layout::make(n, m, comm.size(), comm.rank());
   GJ_REQUIRE(L_.Nr < (int64_t(1) << 31), "too many block rows");
   // auto depth: profiles/small_n_sweep.md (N=8192: depth 2 34.6 vs 35.9 ms; N=16384: 4 wins), and
@@ -156,6 +158,18 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   }
 
   comm_.set_timeout(opt_.comm_timeout_s);
+  // Fault injection (tests only) must never pass for a normal run: every active knob is announced
+  // on stderr once per engine and reported in the policy (bench.py / --json carry it).
+  for (const char* var : {"GJ_TEST_ALLOC_FAIL", "GJ_TEST_HANG", "GJ_TEST_CORRUPT", "GJ_TEST_DROP_WAIT"})
+    if (const char* e = std::getenv(var))
+      if (*e) {
+        if (!fault_injection_.empty()) fault_injection_ += " ";
+        fault_injection_ += std::string(var) + "=" + e;
+      }
+  if (!fault_injection_.empty())
+    std::fprintf(stderr, "gj: rank %d: WARNING: FAULT INJECTION ACTIVE (%s): results of this run are "
+                         "deliberately wrong, hung or failed\n",
+                 (int)L_.k, fault_injection_.c_str());
   hang_step_ = injected_step("GJ_TEST_HANG", L_.k);
   corrupt_step_ = injected_step("GJ_TEST_CORRUPT", L_.k);
   if (const char* e = std::getenv("GJ_TEST_DROP_WAIT")) drop_wait_ = std::string(",") + e + ",";
@@ -223,6 +237,7 @@ Engine::Policy Engine::policy() const {
   p.dense_gemm = dense_gemm_;
   p.la_side = la_side_;
   p.pivot = opt_.pivot == PivotRule::Partial ? "partial" : "block-min-inv-norm";
+  p.fault_injection = fault_injection_;
   return p;
 }
 
@@ -321,6 +336,9 @@ void Engine::alloc_work(int64_t wmax) {
   recs_ = static_cast<PivotRec*>(dev_.alloc(sizeof(PivotRec) * L_.p));
   piv_dev_ = static_cast<PivotResult*>(dev_.alloc(sizeof(PivotResult)));
   dscratch_ = static_cast<double*>(dev_.alloc(sizeof(double) * 64));
+  if (opt_.verify)
+    vparts_ = static_cast<uint64_t*>(
+        dev_.alloc(sizeof(uint64_t) * Device::kHashParts * (size_t)npanels() * (size_t)vslots()));
   ihost_len_ = std::max<int64_t>(L_.Nr, 16) * 2 + 16;
   iscratch_ = static_cast<int32_t*>(dev_.alloc(sizeof(int32_t) * ihost_len_));
   piv_host_ = static_cast<PivotResult*>(dev_.alloc_pinned_coherent(sizeof(PivotResult) * kPivSlots));
@@ -361,7 +379,8 @@ void Engine::label_work() {
       {T_, "T"}, {RP_, "RP"}, {T2_, "T2"}, {inv_, "inv"}, {sel_, "sel"}, {inv1_, "inv1"}, {scores_, "scores"},
       {valid_, "valid"}, {pos_, "pos"}, {phys_at_, "phys_at"}, {used_, "used"}, {seq_, "seq"}, {myrec_, "myrec"},
       {sel_done_, "sel_done"}, {recs_, "recs"}, {piv_dev_, "piv_dev"}, {dscratch_, "dscratch"},
-      {iscratch_, "iscratch"}, {piv_host_, "piv_host"}, {ihost_, "ihost"}, {dhost_, "dhost"}};
+      {iscratch_, "iscratch"}, {piv_host_, "piv_host"}, {ihost_, "ihost"}, {dhost_, "dhost"},
+      {vparts_, "vparts"}};
   for (const auto& nv : named)
     if (nv.first) dev_.label(nv.first, nv.second);
 }
@@ -375,7 +394,8 @@ void Engine::free_work() {
                                reinterpret_cast<void**>(&seq_), reinterpret_cast<void**>(&myrec_),
                                reinterpret_cast<void**>(&sel_done_),
                                reinterpret_cast<void**>(&recs_), reinterpret_cast<void**>(&piv_dev_),
-                               reinterpret_cast<void**>(&dscratch_), reinterpret_cast<void**>(&iscratch_)};
+                               reinterpret_cast<void**>(&dscratch_), reinterpret_cast<void**>(&iscratch_),
+                               reinterpret_cast<void**>(&vparts_)};
   for (int i = 0; i < 3; ++i) dptrs.push_back(&At_[i]);
   for (int i = 0; i < 2; ++i) {
     dptrs.push_back(&Rb_[i]);
@@ -557,6 +577,18 @@ double Engine::residual_file(const std::string& path, int nthreads, Status* stat
   return residual_rows(rows.data(), L_.n);
 }
 
+double Engine::result_norm_inf() {
+  GJ_REQUIRE(solved_, "result_norm_inf: solve() first");
+  double local = 0.0;
+  if (L_.nblk > 0) {
+    dev_.row_abs_max(opt_.dtype, out_, L_.npad, L_, dscratch_, S_MAIN);
+    dev_.copy(dhost_, dscratch_, sizeof(double), S_MAIN);
+    dev_.sync_stream(S_MAIN);
+    local = dhost_[0];
+  }
+  return comm_.host_max(dev_, local);
+}
+
 double Engine::norm_inf() {
   dev_.row_abs_max(opt_.dtype, X_, L_.npad, L_, dscratch_, S_MAIN);
   dev_.copy(dhost_, dscratch_, sizeof(double), S_MAIN);
@@ -580,7 +612,7 @@ void Engine::select(int64_t t, const void* Lt, bool full) {
     dev_.set_block_inverse_hint(bi_hint_);
     dev_.block_inverse(opt_.dtype, sel_, L_.m, inv1_, score1_, valid1_, used1_, L1_, thresh, 1, S_SIDE);
     dev_.set_block_inverse_hint(-1);
-    dev_.commit_candidate(opt_.dtype, inv_, inv1_, valid1_, score1_, opt_.pivot_growth, myrec_, L_, S_SIDE);
+    dev_.commit_candidate(opt_.dtype, inv_, inv1_, valid1_, score1_, opt_.pivot_growth_bound(), myrec_, L_, S_SIDE);
     prof_end(PH_PIVOT, pe, S_SIDE);
   } else {
     // The selection runs in the candidate-inverse launch's last workgroup where the kernel family
@@ -636,6 +668,9 @@ void Engine::select(int64_t t, const void* Lt, bool full) {
   piv_host_[par].step = -1;
   dev_.pivot_global(L_.p > 1 ? recs_ : myrec_, (int32_t)L_.p, (int32_t)t, pos_, phys_at_, used_, seq_, piv_dev_,
                     &piv_host_[par], S_SIDE);
+  if (vparts_ && L_.p > 1)  // the gathered records every rank just reduced identically
+    vhash(t / d_, vslot(V_RECS, t % d_), recs_, (int64_t)sizeof(PivotRec) * L_.p, (int64_t)sizeof(PivotRec) * L_.p,
+          1, S_SIDE);
   prof_end(PH_EXCHANGE, pe, S_SIDE);
   dbg_sync();
 }
@@ -682,6 +717,9 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
       // column t after panel v-1 (look-ahead) and steps t0..t-1 of this panel; the pivot rows of
       // those steps enter as 0 without a mask: their later panel columns were moved out (take_rows)
       dev_.wait(S_SIDE, ev_pp_[par][j - 1]);
+      if (vparts_)  // the piece that just arrived, before its first consumer (this column update)
+        vhash(v, vslot(V_PP, j - 1), elem(PP_[par], (j - 1) * m * dm), dm * (int64_t)es, dm * (int64_t)es, m,
+              S_SIDE);
       const int pe = prof_begin(S_SIDE);
       if (rows > 0) {
         // the update writes the new multipliers -X[:, t]^T (segment j of At) as it stores X[:, t]:
@@ -789,6 +827,8 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
     dev_.record(ev_pp_[par][j], S_SIDE);
     dbg_sync();
   }
+  if (vparts_)  // the panel's pivot sequence as SIDE left it (every rank must agree)
+    vhash(v, vslot(V_SEQ, 0), seq_ + t0, (int64_t)sizeof(int32_t) * q, (int64_t)sizeof(int32_t) * q, 1, S_SIDE);
   if (ahead) {  // the panel's pivots, in step order (the first singular step ends the solve)
     cur_phase_ = "pivot search";
     for (int64_t j = 0; j < q; ++j) {
@@ -907,6 +947,9 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
   const int64_t xn0 = has_next ? panel_t0(v + 1) * m : 0;  // the next panel's columns
   const int64_t xn1 = has_next ? (panel_t0(v + 1) + panel_q(v + 1)) * m : 0;
   dev_.wait(S_COMM, ev_pp_[par][q - 1]);  // all panel pieces, multiplier rows and H_t (SIDE)
+  if (vparts_)  // the last step's piece: no column update consumes it, the chunk pass does first
+    vhash(v, vslot(V_PP, q - 1), elem(PP_[par], (q - 1) * m * (int64_t)d_ * m), (int64_t)d_ * m * (int64_t)es,
+          (int64_t)d_ * m * (int64_t)es, m, S_COMM);
   cur_phase_ = "pivot-row broadcast";
   for (int64_t i = 0; i < C; ++i) {
     const int64_t c = (start + i) % C;
@@ -1011,6 +1054,10 @@ void Engine::lookahead_update(int64_t u) {
     // link 0.0669 -> 0.0595 s / 0.0485 -> 0.0431 s against waiting for the whole first chunk
     // (profiles/emu_direct_r3.md)
     dev_.wait(ms, ev_la_[par]);
+    if (vparts_)
+      for (int64_t j = 0; j < q; ++j)
+        vhash(u, vslot(V_LA, j), elem(LA_[par], j * m * (x1 - x0)), (x1 - x0) * (int64_t)esz(),
+              (x1 - x0) * (int64_t)esz(), m, ms);
     const int pe = prof_begin(ms);
     if (rows > 0) {
       // the first column block's new multipliers -X[:, x0:x0+m]^T go straight into segment 0 of
@@ -1049,6 +1096,10 @@ void Engine::big_update(int64_t u) {
     const int64_t c0 = cb0_[c] * m, c1 = cb1_[c] * m, W = c1 - c0;
     const int ms = S_MAIN;
     if (!dropped("b")) dev_.wait(ms, ev_b_[par][c]);
+    if (vparts_)  // what this chunk's update is about to read, segment by segment (one root each)
+      for (int64_t j = 0; j < q; ++j)
+        vhash(u, vslot(V_RB, j, c), rb_chunk(par, c) + j * m * W * (int64_t)esz(), W * (int64_t)esz(),
+              W * (int64_t)esz(), m, ms);
     const int pe = prof_begin(ms);
     int64_t ra[2], rb[2], nr = 0;
     if (has_next && x0 >= c0 && x0 < c1) {
@@ -1115,13 +1166,20 @@ SolveStats Engine::solve_steps() {
     return st;
   }
 
-  // book-keeping arrays: pos = phys_at = identity, used = 0
-  dev_.host_access(ihost_, sizeof(int32_t) * Nr, true);
-  for (int64_t i = 0; i < Nr; ++i) ihost_[i] = (int32_t)i;
+  // book-keeping arrays: pos = phys_at = identity, used = 0, seq = -1 (no pivot yet: every
+  // owner-predicated launch of a step enqueued ahead of its pivot -- the host-free chain -- is a
+  // no-op on every rank if that step finds none, instead of treating block row 0 as the pivot)
+  dev_.host_access(ihost_, sizeof(int32_t) * 2 * Nr, true);
+  for (int64_t i = 0; i < Nr; ++i) {
+    ihost_[i] = (int32_t)i;
+    ihost_[Nr + i] = -1;
+  }
   dev_.copy(pos_, ihost_, sizeof(int32_t) * Nr, S_SIDE);
   dev_.copy(phys_at_, ihost_, sizeof(int32_t) * Nr, S_SIDE);
   dev_.memset0(used_, sizeof(int32_t) * Nr, S_SIDE);
-  dev_.memset0(seq_, sizeof(int32_t) * Nr, S_SIDE);
+  dev_.copy(seq_, ihost_ + Nr, sizeof(int32_t) * Nr, S_SIDE);
+  if (vparts_)
+    dev_.memset0(vparts_, sizeof(uint64_t) * Device::kHashParts * (size_t)npanels() * (size_t)vslots(), S_SIDE);
   dev_.sync_stream(S_SIDE);
 
   st.pivots.assign(Nr, -1);
@@ -1166,11 +1224,91 @@ SolveStats Engine::solve_steps() {
   const double t_end = now_s();
   for (int64_t t = 0; t < Nr; ++t)
     if (st.pivots[t] != t) st.offdiag_pivots++;
+  if (vparts_) verify_hashes(st);  // outside the timed interval; throws VerifyFailed on every rank
   st.host_wait_ms = host_wait * 1e3;
   st.seconds = t_end - t_begin;
   prof_collect(st);
   solved_ = true;
   return st;
+}
+
+// ---------------------------------------------------------------- GJ_VERIFY
+int Engine::vslot(VKind k, int64_t j, int64_t c) const {
+  const int64_t C = (int64_t)cb0_.size();
+  switch (k) {
+    case V_RB: return (int)(c * d_ + j);
+    case V_PP: return (int)(C * d_ + j);
+    case V_LA: return (int)(C * d_ + d_ + j);
+    case V_RECS: return (int)(C * d_ + 2 * d_ + j);
+    default: return (int)(C * d_ + 3 * d_);
+  }
+}
+
+void Engine::vhash(int64_t v, int slot, const void* base, int64_t ld_bytes, int64_t width_bytes, int64_t rows,
+                   int s) {
+  dev_.hash_rows(base, ld_bytes, width_bytes, rows,
+                 vparts_ + ((size_t)v * vslots() + (size_t)slot) * Device::kHashParts, s);
+}
+
+// All-gather the per-slot hashes and compare every rank's with the root's: the first mismatch in
+// step order (pivot records and sequence, then pieces, look-ahead rows, chunk segments in MAIN's
+// order) names where a rank consumed bytes its root never sent -- a read before the data arrived, or
+// a corrupted copy -- which the final residual can only report as "wrong".  Collective; every rank
+// reaches the same verdict.
+void Engine::verify_hashes(const SolveStats& st) {
+  const int64_t P = npanels(), S = vslots(), C = (int64_t)cb0_.size(), p = L_.p;
+  const size_t nparts = (size_t)P * S * Device::kHashParts;
+  std::vector<uint64_t> parts(nparts);
+  dev_.copy(parts.data(), vparts_, sizeof(uint64_t) * nparts, S_MAIN);
+  dev_.sync_stream(S_MAIN);
+  std::vector<uint64_t> mine((size_t)P * S, 0);
+  for (size_t i = 0; i < mine.size(); ++i)
+    for (int g = 0; g < Device::kHashParts; ++g) mine[i] += parts[i * Device::kHashParts + g];
+  std::vector<uint64_t> all(mine.size() * p);
+  comm_.host_allgather(dev_, mine.data(), all.data(), sizeof(uint64_t) * mine.size());
+  auto h = [&](int64_t r, int64_t v, int slot) { return all[(size_t)r * P * S + (size_t)v * S + slot]; };
+  auto owner = [&](int64_t t) { return (t < (int64_t)st.pivots.size() && st.pivots[t] >= 0) ? st.pivots[t] % p : 0; };
+  for (int64_t v = 0; v < P; ++v) {
+    const int64_t t0 = panel_t0(v), q = panel_q(v);
+    const int64_t start = (v + 1 < P) ? chunk_of_[panel_t0(v + 1)] : 0;
+    struct Item { int slot; int64_t step; const char* phase; std::string buffer; int64_t root; const char* stream; };
+    std::vector<Item> order;
+    for (int64_t j = 0; j < q; ++j)
+      order.push_back({vslot(V_RECS, j), t0 + j, "pivot exchange", "gathered pivot records", -1, "SIDE"});
+    order.push_back({vslot(V_SEQ, 0), t0 + q - 1, "pivot search", "pivot sequence of the panel", -1, "SIDE"});
+    for (int64_t j = 0; j < q; ++j)
+      order.push_back({vslot(V_PP, j), t0 + j, j + 1 < q ? "column update" : "pivot-row broadcast",
+                       "panel piece PP[" + std::to_string(v & 1) + "] step " + std::to_string(j), owner(t0 + j),
+                       j + 1 < q ? "SIDE" : "COMM"});
+    for (int64_t j = 0; j < q; ++j)
+      order.push_back({vslot(V_LA, j), t0 + j, "look-ahead update",
+                       "look-ahead rows LA[" + std::to_string(v & 1) + "] step " + std::to_string(j), owner(t0 + j),
+                       "SIDE"});
+    for (int64_t i = 0; i < C; ++i) {
+      const int64_t c = (start + i) % C;
+      for (int64_t j = 0; j < q; ++j)
+        order.push_back({vslot(V_RB, j, c), t0 + j, "trailing update",
+                         "Rb[" + std::to_string(v & 1) + "] chunk " + std::to_string(c) + " segment " +
+                             std::to_string(j),
+                         owner(t0 + j), "MAIN"});
+    }
+    for (const Item& it : order) {
+      // reference value: the root's hash (broadcast buffers), else rank 0's (gathered / agreed state)
+      const int64_t ref = it.root >= 0 ? it.root : 0;
+      std::vector<int64_t> bad;
+      for (int64_t r = 0; r < p; ++r)
+        if (h(r, v, it.slot) != h(ref, v, it.slot)) bad.push_back(r);
+      if (bad.empty()) continue;
+      std::string who;
+      for (int64_t r : bad) who += (who.empty() ? "" : ", ") + std::to_string(r);
+      throw Error(Status::VerifyFailed,
+                  "GJ_VERIFY: step " + std::to_string(it.step) + " (panel " + std::to_string(v) + "), phase " +
+                      it.phase + ", buffer " + it.buffer + (it.root >= 0 ? ", root rank " + std::to_string(it.root)
+                                                                         : ", reference rank 0") +
+                      ": rank(s) [" + who + "] consumed different bytes on stream " + it.stream +
+                      " (first mismatch in step order)");
+    }
+  }
 }
 
 // inv(A)[t, block s_u] = X[s_t, block u]  (derivation: SURVEY-style sweep bookkeeping; verified
@@ -1534,17 +1672,37 @@ double Engine::axb_residual(const double* x, const double* b) {
 // the normwise backward error ||r|| / (||A|| ||x|| + ||b||) <= tol (inf-norms), after max_refine
 // steps, or when the residual stops shrinking
 // (refinement cannot converge: reported, not hidden).
+RhsResult Engine::solve_rhs_device(const double* b, double* x, const void* dev_rows_f64, int64_t ld,
+                                   int max_refine, double tol) {
+  GJ_REQUIRE(dev_rows_f64 || real_local_rows() == 0, "solve_rhs_device: the matrix rows are needed");
+  return solve_rhs_impl(b, x, nullptr, nullptr, dev_rows_f64, ld, max_refine, tol);
+}
+
 RhsResult Engine::solve_rhs(const double* b, double* x, const GenSpec* gen, const double* host_rows,
                             int64_t ld, int max_refine, double tol) {
-  GJ_REQUIRE(solved_, "solve_rhs: solve() first");
   GJ_REQUIRE(gen || host_rows || real_local_rows() == 0,
              "solve_rhs: the matrix (generator or rows) is needed for the fp64 residual");
+  return solve_rhs_impl(b, x, gen, host_rows, nullptr, ld, max_refine, tol);
+}
+
+RhsResult Engine::solve_rhs_impl(const double* b, double* x, const GenSpec* gen, const double* host_rows,
+                                 const void* dev_rows, int64_t ld, int max_refine, double tol) {
+  GJ_REQUIRE(solved_, "solve_rhs: solve() first");
   const int64_t m = L_.m, n = L_.n;
   RhsResult rr;
   void* Aw = dev_.alloc((size_t)std::max<int64_t>(L_.rows, 1) * L_.npad * 8);
   try {
-    if (gen) dev_.generate(DType::F64, Aw, L_, *gen, S_MAIN);
-    else upload_rows_into(Aw, DType::F64, host_rows, ld);
+    if (gen) {
+      dev_.generate(DType::F64, Aw, L_, *gen, S_MAIN);
+    } else if (dev_rows) {  // zero + identity padding, then the real rows device-to-device
+      GenSpec z;
+      z.kind = GenKind::Zero;
+      dev_.generate(DType::F64, Aw, L_, z, S_MAIN);
+      const int64_t real = real_local_rows();
+      if (real > 0) dev_.copy2d(Aw, L_.npad * 8, dev_rows, ld * 8, n * 8, real, S_MAIN);
+    } else {
+      upload_rows_into(Aw, DType::F64, host_rows, ld);
+    }
     dev_.sync_stream(S_MAIN);
     double bn = 0;
     for (int64_t i = 0; i < n; ++i) bn = std::max(bn, std::fabs(b[i]));

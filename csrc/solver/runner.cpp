@@ -43,7 +43,7 @@ void rank_main(const RunConfig& cfg, int rank, Shared& sh, std::shared_ptr<Loopb
     (void)hipSetDevice(d);
     dev.reset(new HipDevice(d));
     if (use_rccl)
-      comm.reset(new RcclComm(ids, cfg.ranks, rank, d));
+      comm.reset(new RcclComm(ids, cfg.ranks, rank, d, cfg.one_comm));
     else if (cfg.ranks == 1)
       comm.reset(new SelfComm());
     else if (async)

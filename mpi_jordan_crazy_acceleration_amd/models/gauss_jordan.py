@@ -16,7 +16,8 @@ import torch
 from .._native import load_native
 
 STATUS = {0: "ok", 1: "singular matrix", 2: "not enough memory", 3: "cannot open", 4: "cannot read",
-          5: "bad arguments", 6: "communication error", 7: "not enough memory for block"}
+          5: "bad arguments", 6: "communication error", 7: "not enough memory for block",
+          8: "verification failed"}
 
 
 class SingularMatrixError(ArithmeticError):
@@ -102,9 +103,8 @@ class GaussJordan:
         return inv
 
 
-    def _inverse_resident(self, A: torch.Tensor) -> torch.Tensor:
-        """Inverse of a CUDA tensor without host round trips: the rows are copied device-to-device
-        into the engine's panel and the result straight back into a new tensor on A's device."""
+    def _engine_resident(self, A: torch.Tensor):
+        """The native engine, solved on a CUDA tensor's rows (copied device-to-device)."""
         if A.ndim != 2 or A.shape[0] != A.shape[1]:
             raise ValueError("A must be square")
         C = load_native()
@@ -122,9 +122,36 @@ class GaussJordan:
             raise SingularMatrixError("singular matrix")
         if st["status"] != 0:
             raise RuntimeError(STATUS.get(st["status"], "error"))
+        return eng, a
+
+    def _inverse_resident(self, A: torch.Tensor) -> torch.Tensor:
+        """Inverse of a CUDA tensor without host round trips: the rows are copied device-to-device
+        into the engine's panel and the result straight back into a new tensor on A's device."""
+        eng, a = self._engine_resident(A)
         out = torch.empty_like(a)
         eng.download_rows_device(out.data_ptr(), out.stride(0))
         return out.to(A.dtype)
+
+    def solve_resident(self, A: torch.Tensor, b, max_refine: int = -1, tol: float = 1e-15):
+        """A x = b for a CUDA tensor A through the engine (Engine::solve_rhs_device): x = inv(A) b by
+        the native GEMV, then iterative refinement with the residual b - A x in fp64 against A's
+        rows (an fp32 inverse refines to fp64 accuracy on a well-conditioned system, as the CLI's
+        --rhs path).  b: an n-vector or an n x k matrix (columns refined one by one).  Returns
+        (x on A's device in A's dtype, info per column)."""
+        eng, _ = self._engine_resident(A)
+        a64 = A.detach().to(torch.float64).contiguous()
+        torch.cuda.synchronize(a64.device)
+        bt = b.detach().to("cpu", torch.float64) if isinstance(b, torch.Tensor) else \
+            torch.as_tensor(np.asarray(b, dtype=np.float64))
+        cols = bt.reshape(bt.shape[0], -1).numpy()
+        xs, infos = [], []
+        for j in range(cols.shape[1]):
+            x, info = eng.solve_rhs_device(np.ascontiguousarray(cols[:, j]), a64.data_ptr(), a64.stride(0),
+                                           int(max_refine), float(tol))
+            xs.append(x)
+            infos.append(info)
+        x = np.stack(xs, axis=1).reshape(bt.shape)
+        return torch.from_numpy(x).to(device=A.device, dtype=A.dtype), infos
 
 
 _HIP_DEVICES: dict = {}
@@ -145,12 +172,15 @@ def solve(A, b, block_size: int = 128, **kw):
     """Solve ``A x = b`` via the block Gauss-Jordan inverse.
 
     A single right-hand side runs the native path (x = inv(A) b on the devices, the GEMV next to
-    the inverse's rows); a matrix of right-hand sides multiplies by the returned inverse."""
+    the inverse's rows, refined in fp64); a matrix of right-hand sides multiplies by the returned
+    inverse on the host path.  A CUDA tensor A stays on its GPU: the engine solves it in place and
+    every right-hand side (vector or matrix columns) goes through Engine::solve_rhs_device, the
+    native GEMV plus fp64 refinement (never a bare ``inv @ b``)."""
     is_torch = isinstance(A, torch.Tensor)
-    if is_torch and A.is_cuda:  # device-resident: inverse on the GPU, x = inv(A) b next to it
-        inv = inverse(A, block_size=block_size, **kw)
-        bt = b if isinstance(b, torch.Tensor) else torch.as_tensor(np.asarray(b))
-        return inv @ bt.to(device=inv.device, dtype=inv.dtype)
+    if is_torch and A.is_cuda:
+        gj = GaussJordan(block_size=block_size, residual="never", **kw)
+        x, _ = gj.solve_resident(A, b)
+        return x
     bn = b.detach().cpu().numpy() if isinstance(b, torch.Tensor) else np.asarray(b, dtype=np.float64)
     if bn.ndim == 1:
         a = A.detach().to("cpu", torch.float64).numpy() if is_torch else np.asarray(A, dtype=np.float64)

@@ -83,29 +83,39 @@ class TorchDistComm:
         return float(t.item())
 
 
-def agree_hw_queues(group=None, need: Optional[int] = None) -> int:
-    """Collective: the smallest hardware-queue count of any rank (runtime_env.effective_hw_queues).
+def agree_comm_mode(group=None, need: Optional[int] = None) -> dict:
+    """Collective: the RCCL communicator schedule every rank will use.
 
-    The two RCCL communicators of a rank (SIDE, COMM) must not share an in-order hardware queue, or
-    a SIDE kernel spinning on a peer can block the COMM kernel that peer waits for (README
-    "Progress of the two communicators").  When some rank has fewer than ``need`` (16) queues,
-    EVERY rank raises the same explained RuntimeError here, before any RCCL communicator exists
-    (reference: collective error agreement, main.cpp:371-381) -- never a hang."""
+    Two communicators (SIDE: pivot records and panel pieces; COMM: row segments) let the pivot chain
+    run ahead of the chunk broadcasts, but their progress argument needs them on different in-order
+    hardware queues (README "Progress of the two communicators"), i.e. ``need`` (16) queues per
+    process.  When any rank has fewer (HIP initialised before the package could raise
+    GPU_MAX_HW_QUEUES, see runtime_env.effective_hw_queues), or any rank sets ``GJ_ONE_COMM=1``,
+    EVERY rank takes the one-communicator schedule (RcclComm one_comm: one program order of
+    collectives, safe on shared queues) -- a slower run, never a refusal and never a hang.  The
+    decision is agreed here, before any RCCL communicator exists, because creating the second
+    communicator is itself collective (reference: collective agreement, main.cpp:371-381).
+
+    Returns ``{"one_comm": bool, "hw_queues": min over ranks, "reason": str}``."""
     from ..runtime_env import MIN_HW_QUEUES, effective_hw_queues
 
     need = MIN_HW_QUEUES if need is None else need
     rank = dist.get_rank(group)
-    counts = [None] * dist.get_world_size(group)
-    dist.all_gather_object(counts, effective_hw_queues(rank), group=group)
-    low = min(counts)
-    if low < need:
-        bad = [r for r, c in enumerate(counts) if c < need]
-        raise RuntimeError(
-            f"GPU_MAX_HW_QUEUES: rank(s) {bad} run with {low} hardware queues per process, the engine's "
-            f"two RCCL communicators need {need} (HIP was initialised before the package could raise it: "
-            f"set GPU_MAX_HW_QUEUES={need} in the environment, or import mpi_jordan_crazy_acceleration_amd "
-            f"before the first CUDA call)")
-    return low
+    forced = os.environ.get("GJ_ONE_COMM", "0") not in ("", "0")
+    mine = (effective_hw_queues(rank), forced)
+    every = [None] * dist.get_world_size(group)
+    dist.all_gather_object(every, mine, group=group)
+    low = min(q for q, _ in every)
+    short = [r for r, (q, _) in enumerate(every) if q < need]
+    asked = [r for r, (_, f) in enumerate(every) if f]
+    if short:
+        reason = (f"rank(s) {short} run with {low} hardware queues per process (< {need}: HIP was "
+                  f"initialised before the package could raise GPU_MAX_HW_QUEUES)")
+    elif asked:
+        reason = f"GJ_ONE_COMM=1 on rank(s) {asked}"
+    else:
+        reason = ""
+    return {"one_comm": bool(short or asked), "hw_queues": low, "reason": reason}
 
 
 def _raise_file_status(st: int, path, what: str = "") -> None:
@@ -139,16 +149,19 @@ class DistributedGaussJordan:
         self.world = dist.get_world_size()
         self.backend = dist.get_backend()
         self.n, self.m, self.dtype = int(n), int(m), dtype
+        self.comm_mode = {"one_comm": False, "hw_queues": None, "reason": ""}
         if self.backend == "nccl":
             if local_rank is None:
                 local_rank = int(os.environ.get("LOCAL_RANK", torch.cuda.current_device()))
             self.local_rank = local_rank
             self.device = C.hip_device(local_rank)
             if self.world > 1:
-                agree_hw_queues()  # every rank fails together before any RCCL communicator exists
+                # every rank takes the same communicator schedule, before any communicator exists
+                self.comm_mode = agree_comm_mode()
                 obj = [[C.rccl_unique_id(), C.rccl_unique_id()] if self.rank == 0 else None]
                 dist.broadcast_object_list(obj, src=0)
-                self.comm = C.rccl_comm(obj[0], self.world, self.rank, local_rank)
+                self.comm = C.rccl_comm(obj[0], self.world, self.rank, local_rank,
+                                        one_comm=self.comm_mode["one_comm"])
             else:
                 self.comm = C.self_comm()
         else:

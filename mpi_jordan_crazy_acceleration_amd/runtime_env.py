@@ -21,9 +21,9 @@ Values already set higher are kept; nothing is ever lowered or raised above 32.
 HIP reads ``GPU_MAX_HW_QUEUES`` once, when it initialises.  A program that initialised HIP before
 importing this package (a torch CUDA call, ``init_process_group(..., device_id=...)``) runs with
 whatever was set then, so the value the process really has is recorded here
-(:func:`effective_hw_queues`), and a multi-rank RCCL job refuses to start on EVERY rank when any
-rank has fewer than 16 (``parallel.dist.agree_hw_queues``; reference: the collective error
-agreement of main.cpp:371-381) instead of running both communicators on shared queues.
+(:func:`effective_hw_queues`), and when any rank of a multi-rank RCCL job has fewer than 16, EVERY
+rank takes the one-communicator schedule (``parallel.dist.agree_comm_mode``; reference: the
+collective agreement of main.cpp:371-381) instead of running two communicators on shared queues.
 """
 from __future__ import annotations
 

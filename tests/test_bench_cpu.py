@@ -173,15 +173,35 @@ def test_cli_check_residual(gj_bin):
     assert "residual:" in r.stdout  # the reference's output is still printed in full
 
 
-def test_bench_hw_queue_shortfall_agreed():
+def test_bench_hw_queue_shortfall_degrades_to_one_comm():
     """One rank runs with too few hardware queues (HIP initialised before the package could raise
-    GPU_MAX_HW_QUEUES; faked by GJ_TEST_HW_QUEUES=1:4): every rank exits 2 with the same explained
-    message before any communicator exists -- never a hang (runtime_env.py, agree_hw_queues)."""
-    out = _ranks(3, "--steps", "1", "--warmup", "0", "--size", "90", "--block", "8",
-                 env_extra={"GJ_TEST_HW_QUEUES": "1:4"}, timeout=120)
-    for rank, (rc, o, e) in enumerate(out):
-        assert rc == 2, (rank, rc, e[-2000:])
-        assert "rank(s) [1] run with 4 hardware queues" in e, e[-2000:]
+    GPU_MAX_HW_QUEUES; faked by GJ_TEST_HW_QUEUES=1:4): every rank agrees on the one-communicator
+    schedule (parallel.dist.agree_comm_mode) and the run COMPLETES -- no refusal, no hang -- with
+    the same residual bits as the two-communicator run; the JSON names the mode and its reason.
+    Also the p > 1 record's extra untimed profiled solve (phases_ms_max, per-rank host waits)."""
+    args = ("--steps", "1", "--warmup", "0", "--size", "90", "--block", "8")
+    low = _ranks(4, *args, env_extra={"GJ_TEST_HW_QUEUES": "1:4"}, timeout=120)
+    ok = _ranks(4, *args, timeout=120)
+    for rank, (rc, o, e) in enumerate(low + ok):
+        assert rc == 0, (rank, rc, e[-2000:])
+    d_low, d_ok = _json_line(low[0][1]), _json_line(ok[0][1])
+    assert d_low["comm_mode"]["one_comm"] is True and d_low["comm_mode"]["hw_queues"] == 4
+    assert "rank(s) [1] run with 4 hardware queues" in d_low["comm_mode"]["reason"]
+    assert d_ok["comm_mode"]["one_comm"] is False
+    assert d_low["residual_inf"] == d_ok["residual_inf"] and d_low["residual_inf"] < 1e-8
+    for d in (d_low, d_ok):
+        assert d["profiled_solve"]["timed"] is False and len(d["profiled_solve"]["seconds_per_rank"]) == 4
+        assert d["phases_ms_max"]["trailing_update"] > 0 and "pivot_search" in d["phases_ms_max"]
+
+
+def test_one_comm_forced_by_env_on_any_rank():
+    """GJ_ONE_COMM=1 on one rank is enough: the mode is agreed, so ranks never disagree on how many
+    communicators to create (a collective)."""
+    out = _ranks(3, "--steps", "1", "--warmup", "0", "--size", "60", "--block", "8",
+                 env_extra={"GJ_ONE_COMM": "1"}, timeout=120)
+    assert all(rc == 0 for rc, _, _ in out), [e[-1000:] for _, _, e in out]
+    d = _json_line(out[0][1])
+    assert d["comm_mode"]["one_comm"] is True and "GJ_ONE_COMM" in d["comm_mode"]["reason"]
 
 
 def test_effective_hw_queues_after_early_hip_init():

@@ -9,6 +9,16 @@ from mpi_jordan_crazy_acceleration_amd.utils import gauss_jordan_reference, gene
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _verify_multi_rank(request, monkeypatch):
+    """Consumption-point hash verification (GJ_VERIFY, Engine::verify_hashes) is on in every
+    multi-rank schedule test of this tier: a rank that consumes a broadcast buffer before it has
+    arrived fails the test with the step, phase, buffer and stream named, not only by the residual."""
+    name = request.node.name
+    if any(k in name for k in ("async", "host_free", "loopback", "direct_bcast", "depth2")):
+        monkeypatch.setenv("GJ_VERIFY", "1")
+
+
 @pytest.mark.parametrize("n,m", [(1000, 128), (517, 60), (64, 64), (300, 256), (10, 12), (40, 1), (1000, 200),
                                  (1536, 256)])
 @pytest.mark.parametrize("gen", ["random", "absdiff"])
@@ -131,6 +141,29 @@ def test_device_resident_inverse_of_cuda_tensor(dtype):
     assert x.is_cuda
     xr = np.linalg.solve(A.double().cpu().numpy(), b.double().cpu().numpy())
     assert np.abs(x.double().cpu().numpy() - xr).max() / np.abs(xr).max() < (1e-8 if dtype == torch.float64 else 5e-2)
+
+
+@pytest.mark.parametrize("k", [1, 3])
+def test_device_resident_fp32_solve_is_refined(k):
+    """gj.solve on an fp32 CUDA tensor goes through Engine::solve_rhs_device: the fp32 inverse's
+    x = inv(A) b refined with fp64 residuals against A's rows, to ~fp64 accuracy on a
+    well-conditioned (randshift) system -- the CLI --rhs path's answer, not a bare fp32 inv @ b."""
+    n = 1500
+    A64 = generate_matrix(n, "randshift", 4)
+    A = torch.from_numpy(A64).float().cuda()
+    rng = np.random.default_rng(9)
+    b = rng.uniform(-1, 1, (n, k)) if k > 1 else rng.uniform(-1, 1, n)
+    x = gj.solve(A, torch.from_numpy(b).float().cuda(), block_size=128, dtype="fp32")
+    assert x.is_cuda and x.dtype == torch.float32 and tuple(x.shape) == b.shape
+    A32 = A.double().cpu().numpy()  # the fp32 matrix the engine saw, exactly
+    _, infos = gj.GaussJordan(block_size=128, dtype="fp32").solve_resident(A, torch.from_numpy(b))
+    for j, info in enumerate(infos):
+        bj = b[:, j] if k > 1 else b
+        assert info["steps"] >= 1 and info["converged"], info
+        assert info["residual"] / np.abs(bj).max() < 1e-12, info
+    # the returned fp32 x is the refined fp64 solution rounded once
+    xr = np.linalg.solve(A32, b)
+    assert np.abs(x.double().cpu().numpy() - xr).max() / np.abs(xr).max() < 1e-6
 
 
 @pytest.mark.parametrize("p", [3, 8])

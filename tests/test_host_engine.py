@@ -231,3 +231,13 @@ def test_host_gemm_batch_matches_torch():
     ops.gemm_batch(prods)
     for (_, _, _, C), r in zip(prods, refs):
         assert (C - r).abs().max().item() < 1e-12
+
+
+def test_unknown_variant_names_fail_loudly(native):
+    """A typo'd GEMM or block-inverse variant name is an error, never a silent default."""
+    with pytest.raises(ValueError, match="unknown GEMM variant"):
+        native.set_gemm_variant("dtva")
+    with pytest.raises(ValueError, match="unknown block-inverse variant"):
+        native.set_block_inverse_variant("pannel")
+    native.set_gemm_variant("auto")
+    native.set_block_inverse_variant("panel")
