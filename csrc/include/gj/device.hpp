@@ -60,6 +60,34 @@ struct GemmExtra {
   // when the pivot chain has CUs of its own (a CU reservation), slower when it must share them
   // (profiles/gemm_stall_r4.md).
   bool dense = false;
+  // Row-block selection (the pivot-chain / deferred split of a panel's column updates, Engine):
+  // only the row blocks b (height rsel_m, b < 64 kRselWords) whose bit b of rsel is set take part;
+  // M counts the selected rows ((set bits) * rsel_m) and the i-th block of M is the i-th set bit.
+  // Rows of A (K-major), C and tneg are addressed through the map; zero rows stay physical.
+  // rsel_m = 0: off.  The GPU path needs the tile height to divide rsel_m (64 | rsel_m).
+  static constexpr int kRselWords = 8;
+  uint64_t rsel[kRselWords] = {};
+  int64_t rsel_m = 0;
+  int64_t rsel_count() const {
+    int64_t c = 0;
+    for (int w = 0; w < kRselWords; ++w) c += __builtin_popcountll(rsel[w]);
+    return c;
+  }
+  // physical row of selected row i (i < rsel_count() * rsel_m)
+  int64_t rsel_row(int64_t i) const {
+    int64_t bl = i / rsel_m;
+    const int64_t off = i - bl * rsel_m;
+    for (int w = 0; w < kRselWords; ++w) {
+      uint64_t x = rsel[w];
+      const int c = __builtin_popcountll(x);
+      if (bl < c) {
+        for (; bl > 0; --bl) x &= x - 1;
+        return (64 * w + __builtin_ctzll(x)) * rsel_m + off;
+      }
+      bl -= c;
+    }
+    return -1;
+  }
 };
 
 // Owner-side piece work fused into Device::owner_edits (all optional; w = 0 / eye = null: none):

@@ -200,6 +200,7 @@ class Engine {
     bool la_side = true;          // look-ahead rows on SIDE (else COMM)
     std::string pivot;            // "block-min-inv-norm" | "partial"
     std::string fault_injection;  // active GJ_TEST_* knobs ("" in every normal run)
+    bool split = false;           // chain / deferred split of the column updates (split_)
   };
   Policy policy() const;
   const std::string& bcast_algo() const { return bcast_algo_; }  // "ring" | "direct"
@@ -287,6 +288,16 @@ class Engine {
   int reserved_cus_ = 0;
   bool dense_gemm_ = false;        // trailing update at 5 workgroups per CU (GemmExtra::dense)
   bool la_side_ = true;            // look-ahead rows on SIDE (else COMM); GJ_LA_SIDE overrides
+  // Chain / deferred split of a panel's column updates (GJ_SPLIT=0 turns it off): the look-ahead
+  // update and the in-panel column updates on the pivot chain (SIDE) cover only the local block rows
+  // that are still pivot candidates when the panel starts (chain_sel_); the rows already used as
+  // pivot rows (defer_sel_) get the same updates later, on COMM ahead of the panel's chunk pass --
+  // they are needed only by MAIN's trailing update.  Bit-identical results (same products, same k
+  // order per row).  Needs 64 | m and <= 512 local blocks (GemmExtra::rsel).
+  bool split_ = false;
+  std::vector<char> used_local_;       // local blocks used as pivot rows so far (host copy)
+  GemmExtra chain_sel_[2], defer_sel_[2];  // by panel parity; rsel_m == 0: panel without a split
+  void deferred_updates(int64_t v);
   double norm_a_ = -1;
 
   // chunk plan (block-column ranges, multiples of d_ blocks so a panel never straddles chunks)

@@ -37,6 +37,7 @@
 #include <cstdlib>
 #include <string>
 #include <type_traits>
+#include <utility>
 
 #include "kernels.hpp"
 
@@ -147,7 +148,27 @@ struct GemmArgs {
   const int32_t* pred;  // GemmExtra::owner_phys: skip unless *pred % pred_p == pred_k
   int64_t pred_p, pred_k;
   bool dense;           // GemmExtra::dense: the 5-workgroups-per-CU LDS-DMA build
+  uint64_t rsel[GemmExtra::kRselWords];  // GemmExtra::rsel / rsel_m: row-block selection
+  int64_t rsel_m;
 };
+
+// GemmExtra::rsel: physical first row of the tile whose logical first row is r (the block height
+// rsel_m is a multiple of the tile height, so a tile never straddles two selected blocks)
+__device__ __forceinline__ int64_t rsel_map(const GemmArgs& g, int64_t r) {
+  int64_t bl = r / g.rsel_m;
+  const int64_t off = r - bl * g.rsel_m;
+#pragma unroll
+  for (int w = 0; w < GemmExtra::kRselWords; ++w) {
+    uint64_t x = g.rsel[w];
+    const int c = __popcll(x);
+    if (bl < c) {
+      for (; bl > 0; --bl) x &= x - 1;
+      return (64 * w + __ffsll((unsigned long long)x) - 1) * g.rsel_m + off;
+    }
+    bl -= c;
+  }
+  return 0;
+}
 
 // GemmExtra::owner_phys: the whole launch is a no-op on ranks that do not own the pivot
 __device__ __forceinline__ bool gemm_skipped(const GemmArgs& g) {
@@ -176,7 +197,10 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, const int tile) {
   __shared__ T ldsB[2][BK][CF::LDB];  // B slices
 
   const int tm = tile / g.tiles_n, tn = tile % g.tiles_n;
-  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  // m0L: the tile's first row among the M rows of the product; m0: its physical row (they differ
+  // only under a row-block selection, GemmExtra::rsel)
+  const int64_t m0L = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t m0 = g.rsel_m > 0 ? rsel_map(g, m0L) : m0L;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -189,7 +213,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, const int tile) {
   const int rlane = wm * TM + MF::rl(lane);  // row within the tile (minus i*16 + rq)
   const int clane = wn * TN + (lane & 15);   // col within the tile (minus j*16)
   // all masks in 32-bit tile-relative form (row/col bounds and the pivot rows/zero columns)
-  const int Mt = (int)((g.M - m0) < BM ? (g.M - m0) : BM);
+  const int Mt = (int)((g.M - m0L) < BM ? (g.M - m0L) : BM);
   const int Nt = (int)((g.N - n0) < BN ? (g.N - n0) : BN);
   const int64_t zlo = g.zc0 - n0, zhi = g.zc1 - n0;
   const int z0 = (int)(zlo < 0 ? 0 : (zlo > BN ? BN : zlo)), z1 = (int)(zhi < 0 ? 0 : (zhi > BN ? BN : zhi));
@@ -235,7 +259,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, const int tile) {
   const int bk_l = tid / BN, bn_l = tid % BN;
   const int ak_l = tid / BM, am_l = tid % BM;
   const bool b_col_ok = (n0 + bn_l) < g.N;
-  const bool a_col_ok = (m0 + am_l) < g.M;
+  const bool a_col_ok = (m0L + am_l) < g.M;
   const int b_voff = (bk_l * ldb + bn_l) * ES;
   const int a_voff = (AL == 1) ? (ak_l * lda + am_l) * ES : 0;
   T ra[CF::PF][CF::SPA], rb[CF::PF][CF::SPB];
@@ -261,7 +285,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, const int tile) {
       for (int e = 0; e < CF::SPA; ++e) {
         const int idx = e * NT + tid;
         const int ii = idx / BK, kk = idx % BK;
-        const bool ok = (k0 + kk) < g.K && (m0 + ii) < g.M;
+        const bool ok = (k0 + kk) < g.K && (m0L + ii) < g.M;
         ra[S][e] = bload<T>(rar, ok ? (ii * lda + kk) * ES : kOOB, 0);
       }
     }
@@ -442,13 +466,22 @@ struct Geo {
 };
 }  // namespace glds
 
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, double* lds_wave_base, int voff) {
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, double* lds_wave_base, int voff, int soff = 0) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16,
-                                           voff, 0, 0, 0);
+                                           voff, soff, 0, 0);
 }
 
 // s_waitcnt vmcnt(P * n) for a runtime n <= 3: the pieces of the n most recent slices may stay in
 // flight (P pieces per slice)
+// f(std::integral_constant<int, I>) for I = B .. E-1, unrolled at compile time
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
 template <int P>
 __device__ __forceinline__ void wait_pieces(int n) {
   static_assert(P == 3 || P == 6, "pieces per slice");
@@ -465,7 +498,12 @@ __device__ __forceinline__ void wait_pieces(int n) {
   }
 }
 
-template <int MODE, int NS, int OCC, int BK>
+// PEEL = 1: the steady-state loop is unrolled over the NS stages (every LDS stage base, fragment
+// offset and DMA destination a compile-time constant), its slices carry no K mask (the partial last
+// slice, if any, takes the masked issue), and each DMA piece is one per-lane offset fixed for the
+// whole launch plus the slice's byte offset in an SGPR (soffset): no per-slice VALU address or mask
+// arithmetic, and a constant vmcnt per slice.
+template <int MODE, int NS, int OCC, int BK, int PEEL = 0>
 __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
   using namespace glds;
   if (gemm_skipped(g)) return;
@@ -588,19 +626,76 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
 
   const int nk = (int)((g.K + BK - 1) / BK);
   const int pro = nk < NS - 1 ? nk : NS - 1;  // slices issued ahead
-  for (int kt = 0; kt < pro; ++kt) issue(kt);
-  wait_pieces<PIECES>(pro - 1);  // slice 0 landed
-  __builtin_amdgcn_s_barrier();
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + NS - 1 < nk) issue(kt + NS - 1);
-    compute(kt);
-    // slice kt+1 must have landed (this wave's pieces); the later issued ones may stay in flight
-    const int last = (kt + NS - 1 < nk ? kt + NS - 1 : nk - 1);
-    wait_pieces<PIECES>(last - (kt + 1) > 0 ? last - (kt + 1) : 0);
-    // every wave's fragment reads of this stage complete before the barrier that lets a wave
-    // refill it (hipcc sinks the last reads' wait below a raw s_barrier; measured free)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if constexpr (PEEL == 0) {
+    for (int kt = 0; kt < pro; ++kt) issue(kt);
+    wait_pieces<PIECES>(pro - 1);  // slice 0 landed
     __builtin_amdgcn_s_barrier();
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + NS - 1 < nk) issue(kt + NS - 1);
+      compute(kt);
+      // slice kt+1 must have landed (this wave's pieces); the later issued ones may stay in flight
+      const int last = (kt + NS - 1 < nk ? kt + NS - 1 : nk - 1);
+      wait_pieces<PIECES>(last - (kt + 1) > 0 ? last - (kt + 1) : 0);
+      // every wave's fragment reads of this stage complete before the barrier that lets a wave
+      // refill it (hipcc sinks the last reads' wait below a raw s_barrier; measured free)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  } else {
+    const int nfull = Kd / BK;  // slices without a K mask
+    int va[BK / 4], vb[BK / 8];
+#pragma unroll
+    for (int h = 0; h < BK / 4; ++h) va[h] = a_ok ? ((wid + 4 * h) * lda + acol) * ES : kOOB;
+#pragma unroll
+    for (int h = 0; h < BK / 8; ++h) vb[h] = b_ok ? ((brow + 8 * h) * ldb + bcol) * ES : kOOB;
+    const int sa_step = __builtin_amdgcn_readfirstlane(BK * lda * ES);
+    const int sb_step = __builtin_amdgcn_readfirstlane(BK * ldb * ES);
+    for (int kt = 0; kt < pro; ++kt) issue(kt);
+    wait_pieces<PIECES>(pro - 1);  // slice 0 landed
+    __builtin_amdgcn_s_barrier();
+    // steady state, NS slices per trip: every slice it issues (up to kt + 2 NS - 2) is full
+    int kt = 0;
+    for (; kt + 2 * NS - 2 < nfull; kt += NS) {
+      static_for<0, NS>([&](auto s_c) {
+        constexpr int S0 = decltype(s_c)::value, SI = (S0 + NS - 1) % NS;
+        double* st = lds + SI * STAGE;
+        const int kn = kt + S0 + NS - 1;
+#pragma unroll
+        for (int h = 0; h < BK / 4; ++h) dma16(ra, st + (wid + 4 * h) * LDA, va[h], kn * sa_step);
+#pragma unroll
+        for (int h = 0; h < BK / 8; ++h) dma16(rb, st + SA + 2 * (wid + 4 * h) * BN, vb[h], kn * sb_step);
+        const double* sa = lds + S0 * STAGE;
+        const double* sb = sa + SA;
+#pragma unroll
+        for (int kk = 0; kk < BK; kk += 4) {
+          double a[MI], b[NJ];
+          const int kr = kk + (lane >> 4);
+          const int sw = (kr & 1) * 16;
+#pragma unroll
+          for (int i = 0; i < MI; ++i) a[i] = sa[kr * LDA + wm * TM + i * 16 + (lane & 15)];
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) b[j] = sb[kr * BN + ((wn * TN + j * 16 + (lane & 15)) ^ sw)];
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) acc[i][j] = MF::op(a[i], b[j], acc[i][j]);
+        }
+        // slice kt + S0 + 1 landed; the NS - 2 newest may stay in flight
+        static_assert(NS == 2 || (NS == 3 && PIECES == 3), "constant waits written for 2 / 3 stages, BK 8");
+        if constexpr (NS == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      });
+    }
+    for (; kt < nk; ++kt) {  // the last slices: the general loop (runtime stage, masked issue)
+      if (kt + NS - 1 < nk) issue(kt + NS - 1);
+      compute(kt);
+      const int last = (kt + NS - 1 < nk ? kt + NS - 1 : nk - 1);
+      wait_pieces<PIECES>(last - (kt + 1) > 0 ? last - (kt + 1) : 0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
   }
 
 #pragma unroll
@@ -633,6 +728,17 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
   }
 }
 
+// GJ_GLDS_PEEL=0/1 or set_glds_peel(): the peeled, stage-unrolled main loop (PEEL template argument)
+static int g_glds_peel = -1;
+static int glds_peel() {
+  if (g_glds_peel < 0) {
+    const char* e = getenv("GJ_GLDS_PEEL");
+    g_glds_peel = e ? (std::atoi(e) != 0) : 0;
+  }
+  return g_glds_peel;
+}
+void set_glds_peel(int on) { g_glds_peel = on ? 1 : 0; }
+
 template <int MODE>
 static void launch_glds(const GemmArgs& a0, hipStream_t s) {
   GemmArgs a = a0;
@@ -660,7 +766,14 @@ static void launch_glds(const GemmArgs& a0, hipStream_t s) {
     return v == "2.5" ? 25 : v == "3.3" ? 33 : 23;
   }();
   const int build = forced ? forced : (a.dense ? 25 : 23);
-  if (build == 25)
+  if (glds_peel()) {
+    if (build == 25)
+      hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 5, 8, 1>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
+    else if (build == 33)
+      hipLaunchKernelGGL((gemm_glds_f64<MODE, 3, 3, 8, 1>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
+    else
+      hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 3, 8, 1>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
+  } else if (build == 25)
     hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 5, 8>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
   else if (build == 33)
     hipLaunchKernelGGL((gemm_glds_f64<MODE, 3, 3, 8>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
@@ -911,6 +1024,11 @@ constexpr int64_t kSmallGridTiles = 512;
 template <typename T, int AL, int MODE>
 static void launch(const GemmArgs& a, hipStream_t s) {
   if (MODE == MODE_RESID) return launch_cfg<T, AL, MODE, CfgBig>(a, s);
+  if (a.rsel_m > 0) {  // row-block selection: register-staged tiles whose height divides the block
+    if (a.rsel_m % CfgNarrow::BM == 0 && !a.latency) return launch_cfg<T, AL, MODE, CfgNarrow>(a, s);
+    if (a.rsel_m % CfgSmall::BM == 0) return launch_cfg<T, AL, MODE, CfgSmall>(a, s);
+    throw Error(Status::BadArgs, "gemm: a row-block selection needs 64 | block height");
+  }
   const int64_t narrow_tiles = ((a.M + CfgNarrow::BM - 1) / CfgNarrow::BM) * ((a.N + CfgNarrow::BN - 1) / CfgNarrow::BN);
   if (a.latency && narrow_tiles < kSmallGridTiles && gemm_variant() != 0)
     return launch_cfg<T, AL, MODE, CfgSmall>(a, s);
@@ -957,6 +1075,8 @@ static void fill_extra(GemmArgs& a, const GemmExtra* ex) {
   a.pred_p = ex ? ex->owner_p : 1;
   a.pred_k = ex ? ex->owner_k : 0;
   a.dense = ex ? ex->dense : false;
+  a.rsel_m = ex ? ex->rsel_m : 0;
+  for (int w = 0; w < GemmExtra::kRselWords; ++w) a.rsel[w] = ex ? ex->rsel[w] : 0;
 }
 
 void gemm(DType dt, int op, int a_kmajor, int64_t M, int64_t N, int64_t K, const void* A,

@@ -174,6 +174,8 @@ PYBIND11_MODULE(_C, mod) {
   mod.def("set_block_inverse_probe", [](uintptr_t p) { kern::set_block_inverse_probe(reinterpret_cast<int32_t*>(p)); },
           "test probe: device int32 buffer (nblk x m) receiving each candidate's pivot row per column; 0 = off");
   mod.def("set_gemm_variant", [](const std::string& v) { kern::set_gemm_variant(kern::gemm_variant_id(v.c_str())); });
+  mod.def("set_glds_peel", [](bool on) { kern::set_glds_peel(on ? 1 : 0); },
+          "fp64 LDS-DMA trailing-update kernel: the peeled, stage-unrolled main loop (GJ_GLDS_PEEL)");
 
   // Kernel-level entry points (raw pointers; used by the per-kernel numerics tests and
   // mpi_jordan_crazy_acceleration_amd.ops).  Every op runs on the MAIN stream and is waited for.
@@ -450,6 +452,7 @@ PYBIND11_MODULE(_C, mod) {
                                d["look_ahead_rows"] = pl.la_side ? "SIDE" : "COMM";
                                d["pivot"] = pl.pivot;
                                if (!pl.fault_injection.empty()) d["fault_injection"] = pl.fault_injection;
+                               d["split"] = pl.split;
                                d["bcast"] = e.eng->bcast_algo();
                                d["bcast_tuning"] = e.comm->bcast_report();
                                d["comm"] = e.comm->describe();

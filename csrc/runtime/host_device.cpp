@@ -53,7 +53,8 @@ void gemm_t(GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const T* A, 
     const int64_t g = *ex.owner_phys;
     if (g < 0 || g % ex.owner_p != ex.owner_k) return;
   }
-  parallel_for(M, nthreads, [&](int64_t i) {
+  parallel_for(M, nthreads, [&](int64_t il) {
+    const int64_t i = ex.rsel_m > 0 ? ex.rsel_row(il) : il;  // GemmExtra::rsel: physical row
     bool zrow = false;
     for (int z = 0; z < ex.nzr; ++z) zrow |= (i >= ex.zr[z] && i < ex.zr[z] + ex.zh);
     std::vector<double> acc(N, 0.0);

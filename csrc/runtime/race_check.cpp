@@ -355,6 +355,21 @@ void gemm_acc(std::vector<Acc>& a, DType dt, GemmOp op, ALayout al, int64_t M, i
               const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, const GemmExtra& ex) {
   const int64_t es = (int64_t)dtype_size(dt);
   if (M <= 0 || N <= 0) return;
+  if (ex.rsel_m > 0) {  // row-block selection: the selected blocks' rows of A, C and tneg only
+    const int64_t h = ex.rsel_m, cols = ex.tneg ? (ex.tneg_cols > 0 ? std::min(ex.tneg_cols, N) : N) : 0;
+    if (K > 0) a.push_back(R(rect(B, ldb, N, K, es), "B"));
+    for (int64_t i = 0; i < M; i += h) {
+      const int64_t r = ex.rsel_row(i);
+      if (K > 0)
+        a.push_back(R(al == ALayout::KMajor ? rect(static_cast<const char*>(A) + r * es, lda, h, K, es)
+                                            : rect(static_cast<const char*>(A) + r * lda * es, lda, K, h, es),
+                      "A"));
+      a.push_back(W(rect(static_cast<char*>(C) + r * ldc * es, ldc, N, h, es), "C"));
+      if (ex.tneg) a.push_back(W(rect(static_cast<char*>(ex.tneg) + r * es, ex.ldtneg, h, cols, es), "tneg"));
+    }
+    if (ex.owner_phys) a.push_back(R(span(ex.owner_phys, 4), "owner"));
+    return;
+  }
   if (K > 0) {
     a.push_back(R(al == ALayout::KMajor ? rect(A, lda, M, K, es) : rect(A, lda, K, M, es), "A"));
     a.push_back(R(rect(B, ldb, N, K, es), "B"));

@@ -217,6 +217,8 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   if (const char* e = std::getenv("GJ_LA_SIDE")) la_side_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("GJ_HOST_FREE")) host_free_multi_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("GJ_COMM_SMALL_TILES")) comm_small_tiles_ = std::atoi(e) != 0;
+  split_ = L_.m % 64 == 0 && L_.nblk <= 64 * GemmExtra::kRselWords && L_.nblk > 0;
+  if (const char* e = std::getenv("GJ_SPLIT")) split_ = split_ && std::atoi(e) != 0;
 
 }
 
@@ -238,6 +240,7 @@ Engine::Policy Engine::policy() const {
   p.la_side = la_side_;
   p.pivot = opt_.pivot == PivotRule::Partial ? "partial" : "block-min-inv-norm";
   p.fault_injection = fault_injection_;
+  p.split = split_;
   return p;
 }
 
@@ -725,12 +728,15 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
         // the update writes the new multipliers -X[:, t]^T (segment j of At) as it stores X[:, t]:
         // one launch fewer per step (emulated p = 4, N = 16384, direct 50 GB/s: 0.0533 / 0.0538 ->
         // 0.0518 / 0.0518 s; neutral elsewhere, profiles/side_chain_r3.md)
-        GemmExtra ex;
+        // (split_: the rows still candidates at the panel's start; the others in deferred_updates)
+        GemmExtra ex = chain_sel_[par];
         ex.latency = true;
         ex.tneg = Lt;
         ex.ldtneg = rows;
-        dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, m, j * m, At_[v % 3], rows,
-                  elem(PP_[par], j * m), dm, elem(X_, t * m), npad, S_SIDE, ex);
+        const int64_t M = ex.rsel_m > 0 ? ex.rsel_count() * m : rows;
+        if (M > 0)
+          dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, M, m, j * m, At_[v % 3], rows,
+                    elem(PP_[par], j * m), dm, elem(X_, t * m), npad, S_SIDE, ex);
       }
       prof_end(PH_COLUMN, pe, S_SIDE);
       select(t, Lt);
@@ -864,6 +870,7 @@ bool Engine::await_step(int64_t v, int64_t j, SolveStats& st, double& host_wait,
   st.pivots[t] = r.phys;
   if (r.owner == L_.k) {
     --live_;  // this rank's block row s_t is no longer a candidate
+    used_local_[(size_t)(r.phys / L_.p)] = 1;
     st.bcast_bytes += double(L_.m) * L_.npad * esz();
   }
   return true;
@@ -950,6 +957,7 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
   if (vparts_)  // the last step's piece: no column update consumes it, the chunk pass does first
     vhash(v, vslot(V_PP, q - 1), elem(PP_[par], (q - 1) * m * (int64_t)d_ * m), (int64_t)d_ * m * (int64_t)es,
           (int64_t)d_ * m * (int64_t)es, m, S_COMM);
+  deferred_updates(v);
   cur_phase_ = "pivot-row broadcast";
   for (int64_t i = 0; i < C; ++i) {
     const int64_t c = (start + i) % C;
@@ -1030,6 +1038,40 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
   dbg_sync();
 }
 
+// The split_ half that left the pivot chain: for the rows already used as pivot rows when panel v
+// started, panel v-1's look-ahead update of panel v's columns (with its -X^T segment 0 of At) and
+// panel v's in-panel column updates (segments 1..q-1), on COMM right after the last panel piece and
+// ahead of the panel's chunk pass (so ahead of MAIN's trailing update, the only reader of these
+// rows' multipliers).  The products and their k order are the chain's, row for row.
+void Engine::deferred_updates(int64_t v) {
+  const int par = (int)(v & 1);
+  const GemmExtra& sel = defer_sel_[par];
+  if (v == 0 || sel.rsel_m == 0 || L_.rows == 0) return;
+  const int64_t cnt = sel.rsel_count();
+  if (cnt == 0) return;
+  const int64_t m = L_.m, rows = L_.rows, npad = L_.npad, dm = (int64_t)d_ * m, M = cnt * m;
+  const int64_t q = panel_q(v), x0 = panel_t0(v) * m, qp = panel_q(v - 1);
+  cur_phase_ = "deferred column updates";
+  const int pe = prof_begin(S_COMM);
+  GemmExtra ex = pivot_rows_extra((int)((v - 1) & 1), qp);
+  std::copy(sel.rsel, sel.rsel + GemmExtra::kRselWords, ex.rsel);
+  ex.rsel_m = sel.rsel_m;
+  ex.tneg = At_[v % 3];
+  ex.ldtneg = rows;
+  ex.tneg_cols = m;
+  dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, M, q * m, qp * m, At_[(v - 1) % 3], rows,
+            LA_[(v - 1) & 1], q * m, elem(X_, x0), npad, S_COMM, ex);
+  for (int64_t j = 1; j < q; ++j) {
+    GemmExtra ec = sel;
+    ec.latency = true;
+    ec.tneg = elem(At_[v % 3], j * m * rows);
+    ec.ldtneg = rows;
+    dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, M, m, j * m, At_[v % 3], rows, elem(PP_[par], j * m), dm,
+              elem(X_, x0 + j * m), npad, S_COMM, ec);
+  }
+  prof_end(PH_COLUMN, pe, S_COMM);
+}
+
 // First part of panel u's depth-q trailing update: the next panel's block columns (look-ahead), so
 // its pivot search can start; big_update() then does every other chunk on MAIN.  The look-ahead
 // runs on SIDE, right behind the look-ahead rows, not on MAIN: it needs only MAIN's chunk of
@@ -1053,6 +1095,17 @@ void Engine::lookahead_update(int64_t u) {
     // the look-ahead rows of panel u (lookahead_rows): N = 16384 emulated p = 4 / 8 at 50 GB/s per
     // link 0.0669 -> 0.0595 s / 0.0485 -> 0.0431 s against waiting for the whole first chunk
     // (profiles/emu_direct_r3.md)
+    // split_: this update and the next panel's column updates cover the rows still candidates
+    // when panel u+1 starts (every pivot of panel u is known on the host by now); the rows used
+    // before get both in deferred_updates(u + 1) on COMM
+    const int npar = (int)((u + 1) & 1);
+    chain_sel_[npar] = GemmExtra{};
+    defer_sel_[npar] = GemmExtra{};
+    if (split_) {
+      chain_sel_[npar].rsel_m = defer_sel_[npar].rsel_m = m;
+      for (int64_t b = 0; b < L_.nblk; ++b)
+        (used_local_[(size_t)b] ? defer_sel_[npar] : chain_sel_[npar]).rsel[b / 64] |= uint64_t(1) << (b % 64);
+    }
     dev_.wait(ms, ev_la_[par]);
     if (vparts_)
       for (int64_t j = 0; j < q; ++j)
@@ -1067,8 +1120,12 @@ void Engine::lookahead_update(int64_t u) {
       ex.tneg = At_[(u + 1) % 3];
       ex.ldtneg = rows;
       ex.tneg_cols = m;
-      dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, x1 - x0, K, At_[u % 3], rows, LA_[par],
-                x1 - x0, elem(X_, x0), npad, ms, ex);
+      std::copy(chain_sel_[npar].rsel, chain_sel_[npar].rsel + GemmExtra::kRselWords, ex.rsel);
+      ex.rsel_m = chain_sel_[npar].rsel_m;
+      const int64_t M = ex.rsel_m > 0 ? ex.rsel_count() * m : rows;
+      if (M > 0)
+        dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, M, x1 - x0, K, At_[u % 3], rows, LA_[par],
+                  x1 - x0, elem(X_, x0), npad, ms, ex);
     }
     prof_end(PH_UPDATE, pe, ms);
     dev_.record(ev_L_, ms);
@@ -1184,6 +1241,8 @@ SolveStats Engine::solve_steps() {
 
   st.pivots.assign(Nr, -1);
   live_ = L_.nblk;
+  used_local_.assign((size_t)std::max<int64_t>(L_.nblk, 1), 0);
+  for (int i = 0; i < 2; ++i) chain_sel_[i] = defer_sel_[i] = GemmExtra{};
   double host_wait = 0;
   bool ok = true;
 

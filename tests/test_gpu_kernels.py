@@ -215,6 +215,37 @@ def test_gemm_deep_auto_dispatch(native, M, N, K, dtype, variant):
     assert (Cd.cpu().double() - ref).abs().max().item() < tol
 
 
+@pytest.mark.parametrize("M,N,K", [(2948, 2900, 520), (2050, 1030, 516), (1538, 2050, 1003), (4096, 2048, 256),
+                                   (2048, 1024, 8), (1026, 514, 20), (2948, 2902, 16)])
+@pytest.mark.parametrize("build", ["2.3", "2.5"])
+def test_glds_peeled_loop_matches_reference(native, M, N, K, build):
+    """The fp64 LDS-DMA trailing update with the peeled, stage-unrolled main loop (set_glds_peel):
+    K multiple of the 8-deep slice or not (the partial last slice takes the masked issue), too
+    short for a steady-state trip, the 4- and 5-per-CU builds; ragged M / N edges, zero extras."""
+    A = _rand((M, K), torch.float64, 31)
+    B = _rand((K, N), torch.float64, 32)
+    C = _rand((M, N), torch.float64, 33)
+    z0, z1, zr, zh = 128, 256, [0, 1000], 128
+    Cin = C.clone()
+    Cin[:, z0:z1] = 0
+    for r in zr:
+        Cin[r:r + zh] = 0
+    ref = Cin + A @ B
+    outs = []
+    for peel in (0, 1):
+        native.set_glds_peel(peel)
+        try:
+            Cd = C.cuda()
+            ops.gemm(A.t().contiguous().cuda(), B.cuda(), Cd, op="acc", a_kmajor=True, zero_cols=(z0, z1),
+                     zero_rows=zr, zero_row_height=zh, dense=(build == "2.5"))
+            outs.append(Cd.cpu())
+        finally:
+            native.set_glds_peel(0)
+    assert (outs[1].double() - ref).abs().max().item() < 1e-12 * K
+    # same k order, same MFMAs: the peeled loop is bit-identical to the general one
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("count", [1, 3, 4, 6])
 def test_gemm_batch_mixed_store_acc(dtype, count):

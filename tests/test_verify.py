@@ -75,3 +75,43 @@ def test_verify_flag_on_the_cli_and_clean_exit():
                         "random", "300", "12"], capture_output=True, text=True, timeout=180, cwd="/tmp")
     assert r.returncode == 0, r.stderr
     assert "residual:" in r.stdout
+
+
+# ---------------------------------------------------------------- chain / deferred split (Engine::split_)
+def _inv_split(split, n, m, p, depth, comm="async", jitter=200.0, monkeypatch=None, **extra):
+    monkeypatch.setenv("GJ_SPLIT", "1" if split else "0")
+    eng = gj.GaussJordan(block_size=m, ranks=p, device="cpu", comm=comm, depth=depth, jitter_us=jitter,
+                         host_threads=2, extra=dict(verify=True, **extra))
+    rep = eng.run(n, gen="random", seed=8, keep_inverse=True)
+    assert rep["status"] == 0, rep["message"]
+    return rep["inverse"]
+
+
+@pytest.mark.parametrize("p,depth", [(1, 2), (1, 4), (3, 3), (8, 2), (4, 1)])
+def test_split_column_updates_bit_identical(p, depth, monkeypatch):
+    """The look-ahead and in-panel column updates of the rows already used as pivot rows leave the
+    pivot chain (deferred to COMM): the inverse is bit-identical to the unsplit schedule, under
+    jittered asynchronous ranks with consumption-point verification on."""
+    n, m = 64 * 11, 64
+    a = _inv_split(False, n, m, p, depth, monkeypatch=monkeypatch)
+    b = _inv_split(True, n, m, p, depth, monkeypatch=monkeypatch)
+    assert np.array_equal(a, b)
+    A = generate_matrix(n, "random", 8)
+    from mpi_jordan_crazy_acceleration_amd.utils.metrics import residual_ok
+    res = np.abs(A @ b - np.eye(n)).sum(1).max()
+    assert residual_ok(res, n, np.abs(A).sum(1).max(), np.abs(b).sum(1).max()), res
+
+
+def test_split_with_partial_pivoting(monkeypatch):
+    n, m = 64 * 9, 64
+    a = _inv_split(False, n, m, 3, 3, monkeypatch=monkeypatch, pivot="partial")
+    b = _inv_split(True, n, m, 3, 3, monkeypatch=monkeypatch, pivot="partial")
+    assert np.array_equal(a, b)
+
+
+def test_split_policy_reported_and_off_when_not_applicable(native):
+    def pol(m):
+        eng = native.Engine(native.host_device(2), native.self_comm(), 600, m, "fp64")
+        return eng.policy["split"]
+    assert pol(64) is True
+    assert pol(60) is False  # the GPU tiles need 64 | m
