@@ -408,7 +408,7 @@ __global__ __launch_bounds__(256) void block_inverse_generic(const T* __restrict
   }
 }
 
-// Panel-blocked sweep for the large blocks (256 < m <= 2048, fp64 and fp32): reference
+// Panel-blocked sweep for the large blocks (256 < m <= 4096, fp64 and fp32): reference
 // inverse_block (main.cpp:746-820) + block_norm (main.cpp:669-683), same pivot rule as the
 // matrix-core kernels (largest magnitude, ties to the lowest current position under the
 // reference's row swaps).  256 threads; thread tid owns block rows tid + 256 s (s < RPT).
@@ -423,9 +423,10 @@ __global__ __launch_bounds__(256) void block_inverse_generic(const T* __restrict
 //    LDS as [column][PB] so every thread reads the same column: broadcast), i.e. one read-modify-
 //    write pass over the block per PB steps instead of per step, and the panel's own columns
 //    become U + E (same panel algebra as blockinv_mfma.hip).
-// Replaces the per-step global sweep (block_inverse_generic, kept for m > 2048 and as the reference
-// timing of GJ_BI_VARIANT 6).  m > 1024 takes 6 or 8 rows per thread and 4-column panels (the
-// [m][PB] R image + 4 m ints of book-keeping stay within 96 KiB of LDS up to m = 2048).
+// Replaces the per-step global sweep (block_inverse_generic, kept for m > 4096 and as the reference
+// timing of GJ_BI_VARIANT 6).  m > 1024 takes 6 or 8 rows per thread and 4-column panels, m > 2048
+// 12 or 16 rows and 2-column panels (the [m][PB] R image + 4 m ints of book-keeping: <= 128 KiB of
+// the 160 KiB LDS at m = 4096, one workgroup per CU).
 // Branch-free buffer access for the blocked kernel: a masked lane passes an out-of-range offset
 // (load returns 0, store is dropped) — a per-lane branch around a load makes the compiler drain
 // vmcnt at the merge, which serialises the batched loads below.
@@ -487,7 +488,7 @@ __global__ __launch_bounds__(256) void block_inverse_blocked(const T* __restrict
   // every loop over the block below keeps JB independent loads in flight per thread (one wave per
   // SIMD: a load-use chain per element would leave the loop latency-bound); JB x RPT loads in
   // registers, so fewer columns per batch when every thread holds more rows
-  constexpr int JB = RPT > 4 ? 4 : 8;
+  constexpr int JB = RPT > 8 ? 2 : RPT > 4 ? 4 : 8;
   for (int j0 = 0; j0 < m; j0 += JB) {
     T x[JB][RPT];
 #pragma unroll
@@ -716,11 +717,11 @@ template <typename T>
 static bool launch_blocked(const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,
                            const int32_t* used, const Layout& L, double thresh, int64_t nlive, hipStream_t s, void* scratch) {
   const int m = (int)L.m;
-  if (m <= 256 || m > 2048) return false;
+  if (m <= 256 || m > 4096) return false;
   const unsigned grid = (unsigned)(nlive >= 0 ? std::max<int64_t>(nlive, 1) : L.nblk);
   const int live_nblk = nlive >= 0 ? (int)L.nblk : 0;
-  const int RPT = m <= 1024 ? (m + 255) / 256 : m <= 1536 ? 6 : 8;
-  const int PBv = RPT <= 2 ? 16 : RPT <= 4 ? 8 : 4;
+  const int RPT = m <= 1024 ? (m + 255) / 256 : m <= 1536 ? 6 : m <= 2048 ? 8 : m <= 3072 ? 12 : 16;
+  const int PBv = RPT <= 2 ? 16 : RPT <= 4 ? 8 : RPT <= 8 ? 4 : 2;
   const size_t lds = (size_t)m * PBv * sizeof(T) + 4 * (size_t)m * sizeof(int);
   const T* lt = static_cast<const T*>(Lt);
   T* it = static_cast<T*>(inv_t);
@@ -730,8 +731,12 @@ static bool launch_blocked(const void* Lt, int64_t ldl, void* inv_t, double* sco
   do {                                                                                                \
     static bool attr = false;                                                                         \
     if (!attr) {                                                                                      \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&block_inverse_blocked<T, RP, PBB>),    \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);               \
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&block_inverse_blocked<T, RP, PBB>),      \
+                              hipFuncAttributeMaxDynamicSharedMemorySize,                             \
+                              256 * (RP) * ((PBB) * (int)sizeof(T) + 16)) != hipSuccess) {             \
+        (void)hipGetLastError();                                                                      \
+        throw Error(Status::BadArgs, "block inverse: dynamic LDS attribute refused");                 \
+      }                                                                                               \
       attr = true;                                                                                    \
     }                                                                                                 \
     hipLaunchKernelGGL((block_inverse_blocked<T, RP, PBB>), dim3(grid), dim3(256), lds, s, lt, ldl,   \
@@ -741,13 +746,15 @@ static bool launch_blocked(const void* Lt, int64_t ldl, void* inv_t, double* sco
   else if (RPT == 3) GJ_BB(3, 8);
   else if (RPT == 4) GJ_BB(4, 8);
   else if (RPT == 6) GJ_BB(6, 4);
-  else GJ_BB(8, 4);
+  else if (RPT == 8) GJ_BB(8, 4);
+  else if (RPT == 12) GJ_BB(12, 2);
+  else GJ_BB(16, 2);
 #undef GJ_BB
   return true;
 }
 
 // 0 = matrix-core panels (default: blockinv_mfma.hip for 16 < m <= 128, blockinv_big.hip for fp64
-// 128 < m <= 256, the panel-blocked kernel up to 2048), 1 = the per-step register sweep, 5 = the
+// 128 < m <= 256, the panel-blocked kernel up to 4096), 1 = the per-step register sweep, 5 = the
 // co-resident L2-image kernel (fp64 32 < m <= 128; GJ_BI_VARIANT=co), 6 = the per-step global
 // sweep for m > 256 instead of the panel-blocked kernel (reference timing)
 static int g_bi_variant = -1;
@@ -816,7 +823,7 @@ const char* block_inverse_kernel_name(DType dt, int64_t m, int variant) {
   if (v == 0 && m > 16 && m <= 128) return "mfma_register";
   if (v != 1 && f64 && m > 128 && m <= 256) return "l2_image";
   if (m <= 128 || (m <= 256 && !f64)) return "register_sweep";
-  if (v != 6 && m <= 2048) return "panel_blocked";
+  if (v != 6 && m <= 4096) return "panel_blocked";
   return "generic";
 }
 

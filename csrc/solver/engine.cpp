@@ -96,14 +96,18 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // communication-cost model 0.167 vs 0.177 s, while depth 6 / 8 lose at p = 1 / 2 / 4 and at
   // N = 16384: profiles/depth_pgt1.md)
   const bool small_rank = L_.p > 1 && L_.max_nblk * L_.m <= 4096;
-  // Depth 2 stays with one rank: one async-virtual-rank GPU run at p = 8, depth 2 returned a wrong
-  // inverse (profiles/depth_pgt1.md) that the happens-before checker (race_check.hpp) does not
-  // explain -- the schedule matrix of tests/test_race_check.py is race-free -- so p > 1 keeps the
-  // depth the multi-rank tests and the scaling runs have always used.
+  // Depth 2 also on p > 1 ranks of <= 2048 rows (p = 8 at N = 16384, p = 4 at N = 8192): 0.0382
+  // vs 0.0408 s per emulated p = 8 rank at N = 16384 under the direct 50 GB/s model
+  // (profiles/depth_pgt1.md).  It was held back after one round-3 async-virtual-rank run at p = 8,
+  // depth 2 returned a wrong inverse; round 5 re-enabled it once the GPU tier ran that
+  // configuration with consumption-point verification on (GJ_VERIFY, tests/test_gpu_engine.py
+  // test_depth2_p8_async_jittered: every broadcast buffer's bytes checked where it is consumed).
   // (One GPU at N = 32768, depth 8 with the co-resident candidate inverse: 0.9 % faster on one box,
   // 0.5-0.8 % slower on another, same-box A/Bs of round 4 -- not adopted, profiles/rocprof_n32768_r4.md.)
+  const bool tiny_rank = L_.p > 1 && L_.max_nblk * L_.m <= 2048;
   const int want = opt_.depth > 0 ? opt_.depth
-                                  : (L_.p == 1 && L_.npad <= 8192) ? 2 : (small_rank && L_.npad > 16384) ? 8 : 4;
+                   : ((L_.p == 1 && L_.npad <= 8192) || tiny_rank) ? 2
+                   : (small_rank && L_.npad > 16384) ? 8 : 4;
   d_ = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)want, (int64_t)kMaxDepth, L_.Nr}));
 
   // Column chunk plan: fixed partition of the Nr block columns into runs of a multiple of d blocks.

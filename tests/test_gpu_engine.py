@@ -244,10 +244,10 @@ def test_async_ranks_driver_shapes(p, bcast, monkeypatch):
 
 
 @pytest.mark.parametrize("n,m,p", [(1500, 300, 1), (2100, 520, 1), (1800, 300, 3), (2000, 700, 2), (3000, 1100, 1),
-                                   (4200, 2048, 2)])
+                                   (4200, 2048, 2), (6000, 3000, 1), (8192, 4096, 2)])
 @pytest.mark.parametrize("dtype", ["fp64", "fp32"])
 def test_engine_large_blocks(n, m, p, dtype):
-    """256 < m <= 2048: the panel-blocked candidate inverse inside the engine (used blocks skipped,
+    """256 < m <= 4096: the panel-blocked candidate inverse inside the engine (used blocks skipped,
     several pivot steps per rank), one GPU and loopback ranks.  fp64 on the random matrix; fp32 on
     random + sqrt(n) I (the random matrix has kappa ~ 1e7 here: no fp32 inverse of it is accurate,
     BASELINE.md "fp32")."""

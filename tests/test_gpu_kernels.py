@@ -126,6 +126,37 @@ def test_block_inverse(m, dtype, bi_variant):
     assert abs(scores[3].item() - 0.5) < 1e-6
 
 
+@pytest.mark.parametrize("m", [2500, 4096])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_block_inverse_large_m_panel_blocked(native, m, dtype):
+    """2048 < m <= 4096: the panel-blocked kernel with 12 / 16 rows per thread and 2-column panels
+    (was the per-step global sweep), against numpy and against that sweep (the same pivot rule:
+    the inverses and scores agree to rounding)."""
+    nblk = 3
+    rng = np.random.default_rng(m)
+    W = rng.standard_normal((nblk, m, m))
+    if dtype == torch.float32:
+        W += np.sqrt(m) * np.eye(m)  # an fp32 inverse of a random block this size is meaningless
+    W[1] = 0.0
+    X = W.reshape(nblk * m, m)
+    Lt = torch.from_numpy(-X.T.copy()).to(dtype).cuda()
+    inv_t, scores, valid = ops.block_inverse(Lt, nblk * m, m, 1, 0, thresh=1e-12)
+    native.set_block_inverse_variant("generic")
+    try:
+        inv_g, scores_g, valid_g = ops.block_inverse(Lt, nblk * m, m, 1, 0, thresh=1e-12)
+    finally:
+        native.set_block_inverse_variant("panel")
+    assert valid.cpu().tolist() == [1, 0, 1] and valid_g.cpu().tolist() == [1, 0, 1]
+    tol = 1e-9 if dtype == torch.float64 else 1e-4
+    for b in (0, 2):
+        ref = np.linalg.inv(W[b].astype(np.float32 if dtype == torch.float32 else np.float64).astype(np.float64))
+        got = inv_t[b].cpu().double().numpy().T
+        assert np.abs(got - ref).max() / np.abs(ref).max() < tol
+        gen = inv_g[b].cpu().double().numpy().T
+        assert np.abs(got - gen).max() / np.abs(gen).max() < tol
+        assert abs(scores[b].item() - scores_g[b].item()) <= tol * scores_g[b].item()
+
+
 def test_permute_blocks():
     m, nblk, Nr = 32, 3, 5
     X = _rand((nblk * m, Nr * m), torch.float64, 9).cuda()
