@@ -65,6 +65,10 @@ struct GemmExtra {
   // M counts the selected rows ((set bits) * rsel_m) and the i-th block of M is the i-th set bit.
   // Rows of A (K-major), C and tneg are addressed through the map; zero rows stay physical.
   // rsel_m = 0: off.  The GPU path needs the tile height to divide rsel_m (64 | rsel_m).
+  // GemmOp::Acc reading its input from another array: C = C_in (+ masks) + A B, C_in with its own
+  // leading dimension (the owner's pivot-row normalisation, X row -> temp, without a separate copy)
+  const void* c_in = nullptr;
+  int64_t ldc_in = 0;
   static constexpr int kRselWords = 8;
   uint64_t rsel[kRselWords] = {};
   int64_t rsel_m = 0;

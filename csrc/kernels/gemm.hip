@@ -150,6 +150,8 @@ struct GemmArgs {
   bool dense;           // GemmExtra::dense: the 5-workgroups-per-CU LDS-DMA build
   uint64_t rsel[GemmExtra::kRselWords];  // GemmExtra::rsel / rsel_m: row-block selection
   int64_t rsel_m;
+  const void* cin;      // GemmExtra::c_in (MODE_ACC input array, ld ldcin; null: C itself)
+  int64_t ldcin;
 };
 
 // GemmExtra::rsel: physical first row of the tile whose logical first row is r (the block height
@@ -229,12 +231,17 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, const int tile) {
 
   acc_t acc[MI][NJ];
   if (MODE == MODE_ACC) {
+    // the accumulator's input: C itself, or GemmExtra::c_in
+    const int ldi = g.cin ? (int)g.ldcin : ldc;
+    const __amdgpu_buffer_rsrc_t rci =
+        g.cin ? rsrc(static_cast<const T*>(g.cin) + m0 * g.ldcin + n0) : rc;
+    const int civoff = (rlane * ldi + clane) * ES;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int r = rlane + i * 16 + MF::rq(q);
-        const int soff = (i * 16 + MF::rq(q)) * ldc * ES;
+        const int soff = (i * 16 + MF::rq(q)) * ldi * ES;
         bool zrow = false;
 #pragma unroll
         for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) zrow |= (r >= zr0[z] && r < zr1[z]);
@@ -242,7 +249,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, const int tile) {
         for (int j = 0; j < NJ; ++j) {
           const int c = clane + j * 16;
           const bool ok = r < Mt && c < Nt && !zrow && !(c >= z0 && c < z1);
-          acc[i][j][q] = bload<T>(rc, ok ? cvoff + j * 16 * ES : kOOB, soff);
+          acc[i][j][q] = bload<T>(rci, ok ? civoff + j * 16 * ES : kOOB, soff);
         }
       }
   } else {
@@ -1032,6 +1039,7 @@ static void launch(const GemmArgs& a, hipStream_t s) {
   const int64_t narrow_tiles = ((a.M + CfgNarrow::BM - 1) / CfgNarrow::BM) * ((a.N + CfgNarrow::BN - 1) / CfgNarrow::BN);
   if (a.latency && narrow_tiles < kSmallGridTiles && gemm_variant() != 0)
     return launch_cfg<T, AL, MODE, CfgSmall>(a, s);
+  if (a.cin) return launch_cfg<T, AL, MODE, CfgNarrow>(a, s);  // C_in: register-staged tiles only
   int v = gemm_variant();
   if (v == kAutoVariant) {
     // Trailing updates (K >= 256) with enough 128x128 tiles to fill the chip: fp64 the LDS-DMA
@@ -1076,6 +1084,8 @@ static void fill_extra(GemmArgs& a, const GemmExtra* ex) {
   a.pred_k = ex ? ex->owner_k : 0;
   a.dense = ex ? ex->dense : false;
   a.rsel_m = ex ? ex->rsel_m : 0;
+  a.cin = ex ? ex->c_in : nullptr;
+  a.ldcin = ex ? ex->ldc_in : 0;
   for (int w = 0; w < GemmExtra::kRselWords; ++w) a.rsel[w] = ex ? ex->rsel[w] : 0;
 }
 

@@ -65,9 +65,10 @@ void gemm_t(GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const T* A, 
       for (int64_t j = 0; j < N; ++j) acc[j] += a * (double)b[j];
     }
     T* c = C + i * ldc;
+    const T* ci = ex.c_in ? static_cast<const T*>(ex.c_in) + i * ex.ldc_in : c;  // GemmExtra::c_in
     if (op == GemmOp::Acc)
       for (int64_t j = 0; j < N; ++j)
-        c[j] = (T)((zrow || (j >= ex.zc0 && j < ex.zc1) ? 0.0 : (double)c[j]) + acc[j]);
+        c[j] = (T)((zrow || (j >= ex.zc0 && j < ex.zc1) ? 0.0 : (double)ci[j]) + acc[j]);
     else
       for (int64_t j = 0; j < N; ++j) c[j] = (T)acc[j];
     if (ex.tneg) {

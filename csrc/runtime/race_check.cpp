@@ -365,6 +365,8 @@ void gemm_acc(std::vector<Acc>& a, DType dt, GemmOp op, ALayout al, int64_t M, i
                                             : rect(static_cast<const char*>(A) + r * lda * es, lda, K, h, es),
                       "A"));
       a.push_back(W(rect(static_cast<char*>(C) + r * ldc * es, ldc, N, h, es), "C"));
+      if (ex.c_in)
+        a.push_back(R(rect(static_cast<const char*>(ex.c_in) + r * ex.ldc_in * es, ex.ldc_in, N, h, es), "C_in"));
       if (ex.tneg) a.push_back(W(rect(static_cast<char*>(ex.tneg) + r * es, ex.ldtneg, h, cols, es), "tneg"));
     }
     if (ex.owner_phys) a.push_back(R(span(ex.owner_phys, 4), "owner"));
@@ -376,6 +378,7 @@ void gemm_acc(std::vector<Acc>& a, DType dt, GemmOp op, ALayout al, int64_t M, i
   }
   (void)op;  // C += AB reads C too; a write of the same bytes already conflicts with any access
   a.push_back(W(rect(C, ldc, N, M, es), "C"));
+  if (ex.c_in) a.push_back(R(rect(ex.c_in, ex.ldc_in, N, M, es), "C_in"));
   if (ex.tneg) {
     const int64_t cols = ex.tneg_cols > 0 ? std::min(ex.tneg_cols, N) : N;
     a.push_back(W(rect(ex.tneg, ex.ldtneg, M, cols, es), "tneg"));

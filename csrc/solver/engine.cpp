@@ -926,9 +926,12 @@ void Engine::lookahead_rows(int64_t v, bool wait_main) {
           dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, wla, m, Ht_[par][j], m,
                     elem(X_, sl * m * npad + xa), npad, seg, wla, ls, lat);
         } else {
-          dev_.copy2d(Tl, wla * es, elem(X_, sl * m * npad + xa), npad * es, wla * es, m, ls);
+          // Tl = X[s_t, next panel] + Lrow_t LA[earlier steps] (C_in: no separate copy launch)
+          GemmExtra li = lat;
+          li.c_in = elem(X_, sl * m * npad + xa);
+          li.ldc_in = npad;
           dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, m, wla, j * m, Lrow_[par][j], m, LA_[par], wla,
-                    Tl, wla, ls, lat);
+                    Tl, wla, ls, li);
           dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, wla, m, Ht_[par][j], m, Tl, wla, seg, wla,
                     ls, lat);
         }
@@ -1015,9 +1018,11 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
             dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, w, m, Ht_[par][j], m,
                       elem(X_, sl * m * npad + a), npad, seg + (a - c0) * (int64_t)es, W, S_COMM, lat);
           } else {
-            dev_.copy2d(T_, W * es, elem(X_, sl * m * npad + a), npad * es, w * es, m, S_COMM);
+            GemmExtra li = lat;  // T = X[s_t, range] + Lrow_t R[earlier steps] (C_in: no copy launch)
+            li.c_in = elem(X_, sl * m * npad + a);
+            li.ldc_in = npad;
             dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, m, w, j * m, Lrow_[par][j], m,
-                      chunk + (a - c0) * (int64_t)es, W, T_, W, S_COMM, lat);
+                      chunk + (a - c0) * (int64_t)es, W, T_, W, S_COMM, li);
             dev_.gemm(opt_.dtype, GemmOp::Store, ALayout::KMajor, m, w, m, Ht_[par][j], m, T_, W,
                       seg + (a - c0) * (int64_t)es, W, S_COMM, lat);
           }

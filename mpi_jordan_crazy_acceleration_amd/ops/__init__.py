@@ -38,7 +38,8 @@ def _p(t: torch.Tensor) -> int:
 
 def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, op: str = "acc", a_kmajor: bool = False,
          zero_cols=(0, 0), zero_rows=(), zero_row_height: int = 0, tneg: torch.Tensor = None,
-         latency: bool = False, dense: bool = False) -> torch.Tensor:
+         latency: bool = False, dense: bool = False, c_in: torch.Tensor = None, row_blocks=None,
+         row_block_m: int = 0) -> torch.Tensor:
     """C += A@B (op="acc") or C = A@B (op="store").  With a_kmajor, ``A`` is given as A^T (K x M).
 
     Elimination extras (op="acc"): C enters as 0 in the columns ``zero_cols`` = (c0, c1) and in the
@@ -46,7 +47,10 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, op: str = "acc", a_k
     Nt <= N, unit column stride): also receives -C^T of C's first Nt columns, the multiplier panel
     the engine's column / look-ahead updates write as they store C.  ``latency``: the small-tile
     launch the pivot chain uses.  ``dense``: the 5-workgroups-per-CU build of the fp64 LDS-DMA
-    trailing update (the engine's choice under a CU reservation)."""
+    trailing update (the engine's choice under a CU reservation).  ``c_in`` (op="acc"): the
+    accumulator's input array instead of C itself (C = c_in + A@B).  ``row_blocks`` with
+    ``row_block_m``: only those row blocks of C / A^T take part (GemmExtra::rsel); M = C's rows is
+    then the physical height and the product runs over len(row_blocks) * row_block_m rows."""
     assert A.dtype == B.dtype == C.dtype and A.stride(-1) == 1 and B.stride(-1) == 1 and C.stride(-1) == 1
     M, N = C.shape
     K = A.shape[0] if a_kmajor else A.shape[1]
@@ -54,9 +58,16 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, op: str = "acc", a_k
     if tneg is not None:
         assert tneg.dtype == C.dtype and tneg.shape[1] == M and 0 < tneg.shape[0] <= N and tneg.stride(-1) == 1
         tp, ldt, tcols = _p(tneg), tneg.stride(0), tneg.shape[0]
-    device_for(C).gemm(_DT[C.dtype], op, a_kmajor, M, N, K, _p(A), A.stride(0), _p(B), B.stride(0), _p(C), C.stride(0),
-                       int(zero_cols[0]), int(zero_cols[1]), [int(r) for r in zero_rows], int(zero_row_height),
-                       tp, ldt, bool(latency), tcols, bool(dense))
+    cp, ldci = 0, 0
+    if c_in is not None:
+        assert c_in.dtype == C.dtype and c_in.shape == C.shape and c_in.stride(-1) == 1
+        cp, ldci = _p(c_in), c_in.stride(0)
+    rb = [int(b) for b in (row_blocks or [])]
+    Msel = len(rb) * int(row_block_m) if row_block_m else M
+    device_for(C).gemm(_DT[C.dtype], op, a_kmajor, Msel, N, K, _p(A), A.stride(0), _p(B), B.stride(0), _p(C),
+                       C.stride(0), int(zero_cols[0]), int(zero_cols[1]), [int(r) for r in zero_rows],
+                       int(zero_row_height), tp, ldt, bool(latency), tcols, bool(dense), cp, ldci, rb,
+                       int(row_block_m))
     return C
 
 

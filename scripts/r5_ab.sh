@@ -33,3 +33,10 @@ done
 for p in 0 1; do
   GJ_GLDS_PEEL=$p timeout -k 10 200 python bench.py --size 8192 --steps 10 --warmup 2 --no-residual > $o/b.json 2>&1 && python3 -c "import json; d=json.loads(open('$o/b.json').read().splitlines()[-1]); print('n=8192 peel=$p', d['ms_per_step'])"
 done
+# emulated p = 8 / 4 ranks at N = 16384 (the 2048 / 4096-row ranks), auto depth (2 on the
+# 2048-row rank since round 5) against depth 4, split on / off: rank-0 time, comm-free and the
+# direct-broadcast 50 GB/s model
+for s in 1 0; do
+  GJ_SPLIT=$s timeout -k 10 300 python bench/bench_emulate.py --ranks 8 4 --size 16384 --depth 0 4 --bw 50 --bcast direct --reps 2 > $o/emu_$s.txt 2>&1 || exit $?
+  echo "== emulate split=$s"; tail -12 $o/emu_$s.txt
+done

@@ -157,6 +157,36 @@ def test_block_inverse_large_m_panel_blocked(native, m, dtype):
         assert abs(scores[b].item() - scores_g[b].item()) <= tol * scores_g[b].item()
 
 
+@pytest.mark.parametrize("m,blocks,latency", [(64, [0, 2, 3, 7], True), (128, [1, 4], False), (128, [0], True),
+                                              (64, list(range(8)), False)])
+@pytest.mark.parametrize("c_in", [False, True])
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_gemm_row_blocks_and_c_in(m, blocks, latency, c_in, dtype):
+    """GemmExtra::rsel (the split pivot chain's row-selected column updates) and GemmExtra::c_in (the
+    owners' normalisation input without a copy): only the selected row blocks of C and -C^T change,
+    with C_in + A B; the others keep their bytes.  Same k order as the full product: bit-identical
+    rows."""
+    M, N, K = 8 * m, 192, 3 * m
+    A = _rand((M, K), torch.float64, 41).to(dtype).cuda()
+    B = _rand((K, N), torch.float64, 42).to(dtype).cuda()
+    C = _rand((M, N), torch.float64, 43).to(dtype).cuda()
+    Ci = _rand((M, N), torch.float64, 44).to(dtype).cuda() if c_in else None
+    T = torch.full((m, M), 5.0, dtype=dtype, device="cuda")
+    full = (Ci if c_in else C).clone()
+    Tf = T.clone()
+    ops.gemm(A.t().contiguous(), B, full, op="acc", a_kmajor=True, tneg=Tf, latency=latency)
+    got = C.clone()
+    ops.gemm(A.t().contiguous(), B, got, op="acc", a_kmajor=True, tneg=T, latency=latency, c_in=Ci,
+             row_blocks=blocks, row_block_m=m)
+    sel = torch.zeros(M, dtype=torch.bool)
+    for b in blocks:
+        sel[b * m:(b + 1) * m] = True
+    sel = sel.cuda()
+    assert torch.equal(got[sel], full[sel])
+    assert torch.equal(got[~sel], C[~sel])
+    assert torch.equal(T[:, sel], Tf[:, sel]) and bool((T[:, ~sel] == 5.0).all())
+
+
 def test_permute_blocks():
     m, nblk, Nr = 32, 3, 5
     X = _rand((nblk * m, Nr * m), torch.float64, 9).cuda()
