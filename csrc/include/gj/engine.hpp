@@ -288,7 +288,8 @@ class Engine {
   int reserved_cus_ = 0;
   bool dense_gemm_ = false;        // trailing update at 5 workgroups per CU (GemmExtra::dense)
   bool la_side_ = true;            // look-ahead rows on SIDE (else COMM); GJ_LA_SIDE overrides
-  // Chain / deferred split of a panel's column updates (GJ_SPLIT=0 turns it off): the look-ahead
+  // Chain / deferred split of a panel's column updates (opt-in, GJ_SPLIT=1; measured slower by
+  // default, profiles/split_r5.md): the look-ahead
   // update and the in-panel column updates on the pivot chain (SIDE) cover only the local block rows
   // that are still pivot candidates when the panel starts (chain_sel_); the rows already used as
   // pivot rows (defer_sel_) get the same updates later, on COMM ahead of the panel's chunk pass --

@@ -735,16 +735,35 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
   }
 }
 
-// GJ_GLDS_PEEL=0/1 or set_glds_peel(): the peeled, stage-unrolled main loop (PEEL template argument)
+// GJ_GLDS_PEEL=0/1 or set_glds_peel(): the peeled, stage-unrolled main loop (PEEL template
+// argument; default on since round 5).  32768 x 8192 x 512 alone, one box: 2 stages 63.65 -> 66.56
+// TF/s, 3 stages 61.24 -> 67.57; the N = 32768 solve 1139 -> 1114 (2 stages) -> 1092-1093 ms
+// (3 stages), two repetitions (scripts/r5_ab.sh, profiles/gemm_peel_r5.md).
 static int g_glds_peel = -1;
 static int glds_peel() {
   if (g_glds_peel < 0) {
     const char* e = getenv("GJ_GLDS_PEEL");
-    g_glds_peel = e ? (std::atoi(e) != 0) : 0;
+    g_glds_peel = e ? (std::atoi(e) != 0) : 1;
   }
   return g_glds_peel;
 }
 void set_glds_peel(int on) { g_glds_peel = on ? 1 : 0; }
+// GJ_GLDS_BUILD=<stages>.<waves-per-SIMD bound> (2.3 | 2.5 | 3.3) or set_glds_build(23 | 25 | 33):
+// one build for every launch (A/B runs, tests); 0 = auto
+static int g_glds_build = -1;
+static int glds_build_forced() {
+  if (g_glds_build < 0) {
+    const char* e = getenv("GJ_GLDS_BUILD");
+    const std::string v = e ? e : "";
+    g_glds_build = v.empty() ? 0 : v == "2.5" ? 25 : v == "3.3" ? 33 : v == "2.3" ? 23 : -2;
+    if (g_glds_build == -2) throw std::invalid_argument("GJ_GLDS_BUILD: 2.3 | 2.5 | 3.3");
+  }
+  return g_glds_build;
+}
+void set_glds_build(int b) {
+  if (b != 0 && b != 23 && b != 25 && b != 33) throw std::invalid_argument("glds build: 0 | 23 | 25 | 33");
+  g_glds_build = b;
+}
 
 template <int MODE>
 static void launch_glds(const GemmArgs& a0, hipStream_t s) {
@@ -763,16 +782,12 @@ static void launch_glds(const GemmArgs& a0, hipStream_t s) {
   // the <2,3,8> schedule is the faster of the two 4-per-CU builds, so it is the only build.  Tile
   // rows are walked in groups of 4 (+0.5-1 %; groups 1-32 measured).
   a.group = 4;
-  // GJ_GLDS_BUILD=<stages>.<waves-per-SIMD bound>: in-solve re-measurement of the residency trade
-  // (the pivot chain got lighter in round 4: no dead candidate-inverse workgroups, no host round
-  // trip per step); 2.3 is the default build
-  static const int forced = [] {
-    const char* e = getenv("GJ_GLDS_BUILD");
-    if (!e) return 0;
-    const std::string v = e;
-    return v == "2.5" ? 25 : v == "3.3" ? 33 : 23;
-  }();
-  const int build = forced ? forced : (a.dense ? 25 : 23);
+  // Round 5: with the peeled loop (constant vmcnt, no per-slice address / mask VALU) the third
+  // stage pays -- it lets a slice's DMA stay in flight across a whole slice of MFMAs -- so 3.3 is
+  // the default at 4 workgroups per CU; under a CU reservation the 5-per-CU build (2 stages: 5 x 3
+  // stages would exceed the LDS) stays.  Without the peel, 2.3 (3.3 was slower, above).
+  const int forced = glds_build_forced();
+  const int build = forced ? forced : a.dense ? 25 : glds_peel() ? 33 : 23;
   if (glds_peel()) {
     if (build == 25)
       hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 5, 8, 1>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);

@@ -176,6 +176,8 @@ PYBIND11_MODULE(_C, mod) {
   mod.def("set_gemm_variant", [](const std::string& v) { kern::set_gemm_variant(kern::gemm_variant_id(v.c_str())); });
   mod.def("set_glds_peel", [](bool on) { kern::set_glds_peel(on ? 1 : 0); },
           "fp64 LDS-DMA trailing-update kernel: the peeled, stage-unrolled main loop (GJ_GLDS_PEEL)");
+  mod.def("set_glds_build", [](int b) { kern::set_glds_build(b); },
+          "fp64 LDS-DMA trailing-update build for every launch: 23 | 25 | 33, 0 = auto (GJ_GLDS_BUILD)");
 
   // Kernel-level entry points (raw pointers; used by the per-kernel numerics tests and
   // mpi_jordan_crazy_acceleration_amd.ops).  Every op runs on the MAIN stream and is waited for.

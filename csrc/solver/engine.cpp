@@ -221,8 +221,14 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   if (const char* e = std::getenv("GJ_LA_SIDE")) la_side_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("GJ_HOST_FREE")) host_free_multi_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("GJ_COMM_SMALL_TILES")) comm_small_tiles_ = std::atoi(e) != 0;
-  split_ = L_.m % 64 == 0 && L_.nblk <= 64 * GemmExtra::kRselWords && L_.nblk > 0;
-  if (const char* e = std::getenv("GJ_SPLIT")) split_ = split_ && std::atoi(e) != 0;
+  // Measured round 5 (scripts/r5_ab.sh, one box, two repetitions): N = 8192 25.35 / 25.49 ->
+  // 25.90 / 25.96 ms, N = 16384 159.6 / 160.7 -> 158.9 / 158.5, N = 32768 1130 / 1131 -> 1139 /
+  // 1139 ms, emulated p = 4 at N = 16384 (direct 50 GB/s) 0.0515 -> 0.0586 s: the deferred half
+  // delays COMM's chunk pass and runs on the same reserved CUs as the chain.  Off by default;
+  // GJ_SPLIT=1 turns it on (profiles/split_r5.md).
+  split_ = false;
+  if (const char* e = std::getenv("GJ_SPLIT"))
+    split_ = std::atoi(e) != 0 && L_.m % 64 == 0 && L_.nblk <= 64 * GemmExtra::kRselWords && L_.nblk > 0;
 
 }
 

@@ -126,8 +126,7 @@ def test_block_inverse(m, dtype, bi_variant):
     assert abs(scores[3].item() - 0.5) < 1e-6
 
 
-@pytest.mark.parametrize("m", [2500, 4096])
-@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("m,dtype", [(2500, torch.float64), (4096, torch.float32)])
 def test_block_inverse_large_m_panel_blocked(native, m, dtype):
     """2048 < m <= 4096: the panel-blocked kernel with 12 / 16 rows per thread and 2-column panels
     (was the per-step global sweep), against numpy and against that sweep (the same pivot rule:
@@ -278,11 +277,12 @@ def test_gemm_deep_auto_dispatch(native, M, N, K, dtype, variant):
 
 @pytest.mark.parametrize("M,N,K", [(2948, 2900, 520), (2050, 1030, 516), (1538, 2050, 1003), (4096, 2048, 256),
                                    (2048, 1024, 8), (1026, 514, 20), (2948, 2902, 16)])
-@pytest.mark.parametrize("build", ["2.3", "2.5"])
+@pytest.mark.parametrize("build", [23, 33, 25])
 def test_glds_peeled_loop_matches_reference(native, M, N, K, build):
     """The fp64 LDS-DMA trailing update with the peeled, stage-unrolled main loop (set_glds_peel):
     K multiple of the 8-deep slice or not (the partial last slice takes the masked issue), too
-    short for a steady-state trip, the 4- and 5-per-CU builds; ragged M / N edges, zero extras."""
+    short for a steady-state trip, every build (2 / 3 stages, 4 and 5 per CU); ragged M / N edges,
+    zero extras.  Bit-identical to the general loop of the same build."""
     A = _rand((M, K), torch.float64, 31)
     B = _rand((K, N), torch.float64, 32)
     C = _rand((M, N), torch.float64, 33)
@@ -293,15 +293,17 @@ def test_glds_peeled_loop_matches_reference(native, M, N, K, build):
         Cin[r:r + zh] = 0
     ref = Cin + A @ B
     outs = []
-    for peel in (0, 1):
-        native.set_glds_peel(peel)
-        try:
+    native.set_glds_build(build)
+    try:
+        for peel in (0, 1):
+            native.set_glds_peel(peel)
             Cd = C.cuda()
             ops.gemm(A.t().contiguous().cuda(), B.cuda(), Cd, op="acc", a_kmajor=True, zero_cols=(z0, z1),
-                     zero_rows=zr, zero_row_height=zh, dense=(build == "2.5"))
+                     zero_rows=zr, zero_row_height=zh, dense=(build == 25))
             outs.append(Cd.cpu())
-        finally:
-            native.set_glds_peel(0)
+    finally:
+        native.set_glds_peel(1)
+        native.set_glds_build(0)
     assert (outs[1].double() - ref).abs().max().item() < 1e-12 * K
     # same k order, same MFMAs: the peeled loop is bit-identical to the general one
     assert torch.equal(outs[0], outs[1])

@@ -109,9 +109,11 @@ def test_split_with_partial_pivoting(monkeypatch):
     assert np.array_equal(a, b)
 
 
-def test_split_policy_reported_and_off_when_not_applicable(native):
+def test_split_policy_reported_and_off_when_not_applicable(native, monkeypatch):
     def pol(m):
         eng = native.Engine(native.host_device(2), native.self_comm(), 600, m, "fp64")
         return eng.policy["split"]
+    assert pol(64) is False  # opt-in (measured slower by default, profiles/split_r5.md)
+    monkeypatch.setenv("GJ_SPLIT", "1")
     assert pol(64) is True
     assert pol(60) is False  # the GPU tiles need 64 | m
