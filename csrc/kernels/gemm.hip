@@ -828,6 +828,10 @@ __device__ __forceinline__ void wait_vm() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+__device__ __forceinline__ void dma16f(__amdgpu_buffer_rsrc_t r, float* lds_wave_base, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, soff,
+                                           0, 0);
+}
 template <int P>
 __device__ __forceinline__ void wait_slices(int n) {  // the pieces of the n newest slices may fly
   if (n <= 0) wait_vm<0>();
@@ -836,7 +840,8 @@ __device__ __forceinline__ void wait_slices(int n) {  // the pieces of the n new
   else wait_vm<3 * P>();
 }
 
-template <int MODE, int NS, int OCC, int BK>
+// PEEL = 1: the fp64 kernel's peeled, stage-unrolled steady state (gemm_glds_f64), for fp32.
+template <int MODE, int NS, int OCC, int BK, int PEEL = 0>
 __global__ __launch_bounds__(glds32::NT, OCC) void gemm_glds_f32(GemmArgs g) {
   using namespace glds32;
   if (gemm_skipped(g)) return;
@@ -934,9 +939,9 @@ __global__ __launch_bounds__(glds32::NT, OCC) void gemm_glds_f32(GemmArgs g) {
     }
   };
   // fragments of k step kk + 2 are read while the MFMAs of step kk run (two register sets)
-  auto compute = [&](int kt) {
-    const float* sa = lds + (kt % NS) * STAGE + wm * TM + (lane & 31) + (lane >> 5) * BM;
-    const float* sb = lds + (kt % NS) * STAGE + SA + wn * TN + (lane & 31) + (lane >> 5) * BN;
+  auto compute_st = [&](const int stage) {
+    const float* sa = lds + stage * STAGE + wm * TM + (lane & 31) + (lane >> 5) * BM;
+    const float* sb = lds + stage * STAGE + SA + wn * TN + (lane & 31) + (lane >> 5) * BN;
     float a[2][MI], b[2][NJ];
     auto frag = [&](int kk, int s) {
 #pragma unroll
@@ -957,13 +962,44 @@ __global__ __launch_bounds__(glds32::NT, OCC) void gemm_glds_f32(GemmArgs g) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s][i], b[s][j], acc[i][j], 0, 0, 0);
     }
   };
+  auto compute = [&](int kt) { compute_st(kt % NS); };
 
   const int nk = (int)((g.K + BK - 1) / BK);
   const int pro = nk < NS - 1 ? nk : NS - 1;
   for (int kt = 0; kt < pro; ++kt) issue(kt);
   wait_slices<PIECES>(pro - 1);
   __builtin_amdgcn_s_barrier();
-  for (int kt = 0; kt < nk; ++kt) {
+  int kt = 0;
+  if constexpr (PEEL == 1) {
+    // steady state, NS slices per trip, every slice it issues (up to kt + 2 NS - 2) full: fixed
+    // per-lane DMA offsets + the slice offset in an SGPR, compile-time stages, constant waits
+    const int nfull = Kd / BK;
+    int va[BK / 8], vb[BK / 8];
+#pragma unroll
+    for (int h = 0; h < BK / 8; ++h) {
+      const int kr = 2 * (wid + 4 * h) + drow;
+      va[h] = a_ok ? (kr * lda + dcol) * ES : kOOB;
+      vb[h] = b_ok ? (kr * ldb + dcol) * ES : kOOB;
+    }
+    const int sa_step = __builtin_amdgcn_readfirstlane(BK * lda * ES);
+    const int sb_step = __builtin_amdgcn_readfirstlane(BK * ldb * ES);
+    for (; kt + 2 * NS - 2 < nfull; kt += NS) {
+      static_for<0, NS>([&](auto s_c) {
+        constexpr int S0 = decltype(s_c)::value, SI = (S0 + NS - 1) % NS;
+        float* st = lds + SI * STAGE;
+        const int kn = kt + S0 + NS - 1;
+#pragma unroll
+        for (int h = 0; h < BK / 8; ++h) dma16f(ra, st + 2 * (wid + 4 * h) * BM, va[h], kn * sa_step);
+#pragma unroll
+        for (int h = 0; h < BK / 8; ++h) dma16f(rb, st + SA + 2 * (wid + 4 * h) * BN, vb[h], kn * sb_step);
+        compute_st(S0);
+        wait_vm<PIECES * (NS - 2)>();  // slice kt + S0 + 1 landed; the NS - 2 newest may fly
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      });
+    }
+  }
+  for (; kt < nk; ++kt) {
     if (kt + NS - 1 < nk) issue(kt + NS - 1);
     compute(kt);
     const int last = (kt + NS - 1 < nk ? kt + NS - 1 : nk - 1);
@@ -1000,7 +1036,24 @@ static void launch_glds32(const GemmArgs& a0, hipStream_t s) {
   // 125.9 / 128.5 / 132.4 (4 WG/CU at 114 VGPRs), <2,2,16> 122.1 / 128.1 / 133.1, <3,2,16> 122.5 /
   // 125.0 / 129.1, <2,3,8> 125.3 / 127.7 / 131.4, <2,2,32> 116.2 / 118.4 / 124.1; squarepf 117.8 /
   // 119.8 / 122.3.
-  hipLaunchKernelGGL((gemm_glds_f32<MODE, 2, 3, 16>), dim3((unsigned)nwg), dim3(glds32::NT), 0, s, a);
+  // Round 5: the peeled steady state (set_glds_peel / GJ_GLDS_PEEL, shared with the fp64 kernel);
+  // GJ_GLDS32_BUILD=2.3 / 2.4 / 3.3 (stages.launch-bound waves): A/B runs.  The peeled 2-stage loop
+  // takes 152 VGPRs under a bound of 3 (3 per CU); 2.4 caps it at 128 for 4 per CU.
+  static const int b32 = [] {
+    const char* e = getenv("GJ_GLDS32_BUILD");
+    const std::string v = e ? e : "";
+    return v == "2.3" ? 23 : v == "3.3" ? 33 : 24;
+  }();
+  if (glds_peel()) {
+    if (b32 == 33)
+      hipLaunchKernelGGL((gemm_glds_f32<MODE, 3, 3, 16, 1>), dim3((unsigned)nwg), dim3(glds32::NT), 0, s, a);
+    else if (b32 == 23)
+      hipLaunchKernelGGL((gemm_glds_f32<MODE, 2, 3, 16, 1>), dim3((unsigned)nwg), dim3(glds32::NT), 0, s, a);
+    else
+      hipLaunchKernelGGL((gemm_glds_f32<MODE, 2, 4, 16, 1>), dim3((unsigned)nwg), dim3(glds32::NT), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((gemm_glds_f32<MODE, 2, 3, 16>), dim3((unsigned)nwg), dim3(glds32::NT), 0, s, a);
+  }
 }
 
 static bool glds32_ok(const GemmArgs& a) {

@@ -141,7 +141,10 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // the reservation at 100 GB/s, p = 2 / 4 are 9 / 6 % slower (profiles/cu_reserve_pgt1.md).
   if (rc < 0) rc = (dev_.on_gpu() && (L_.npad <= 16384 || small_rank)) ? 32 : 0;
   reserved_cus_ = dev_.reserve_cus(rc);
-  dense_gemm_ = reserved_cus_ > 0;
+  // (round 5, peeled loop: at N <= 8192 on one GPU the 3-stage 4-per-CU build is faster even under
+  // the reservation, 25.06 vs 25.43 ms; N = 16384 keeps 5 per CU, 153.9 vs 156.1 ms,
+  // profiles/gemm_peel_r5.md)
+  dense_gemm_ = reserved_cus_ > 0 && !(L_.p == 1 && L_.npad <= 8192);
   if (const char* e = std::getenv("GJ_DENSE_GEMM")) dense_gemm_ = std::atoi(e) != 0;
   // Candidate inverses on ranks whose trailing update holds every CU (p > 1 without a reservation:
   // the 16384- and 8192-row ranks of N = 32768) take the co-resident 4-wave form, which starts in
