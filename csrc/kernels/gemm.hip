@@ -1109,15 +1109,21 @@ static void launch(const GemmArgs& a, hipStream_t s) {
     return launch_cfg<T, AL, MODE, CfgSmall>(a, s);
   if (a.cin) return launch_cfg<T, AL, MODE, CfgNarrow>(a, s);  // C_in: register-staged tiles only
   int v = gemm_variant();
+  int fallback = sizeof(T) == 8 ? 9 : 6;  // when the LDS-DMA kernel cannot take the shape
   if (v == kAutoVariant) {
     // Trailing updates (K >= 256) with enough 128x128 tiles to fill the chip: fp64 the LDS-DMA
     // kernel (61 TF/s vs 57.6 register-staged at 32768x4096x512; at the depth-2 K = 256 of
     // N = 8192 45.6 vs 43.1 TF/s at 8192x4096x256 and 26.9 vs 27.9 ms per inversion, round 3),
     // fp32 (K >= 384, as measured) the LDS-DMA 32x32x2 kernel.  Everything else keeps the
     // register-staged narrow tile.
+    // Round 5, with the peeled LDS-DMA loop: every fp64 non-latency product takes it (the owners'
+    // row normalisations of the chunk pass, the look-ahead update at N <= 16384 too): N = 8192
+    // 25.54 / 24.95 -> 24.65 / 24.54 ms, N = 16384 153.4 / 152.7 -> 152.8 / 152.3, N = 32768 even
+    // (scripts/r5_fp32.sh, profiles/gemm_peel_r5.md).
     const int64_t big_tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
     const bool deep = a.K >= (sizeof(T) == 8 ? 256 : 384) && big_tiles >= 512;
-    v = deep ? 11 : 1;
+    v = (deep || sizeof(T) == 8) ? 11 : 1;
+    if (!deep) fallback = 1;  // the round-4 rule's register-staged narrow tile
   }
   if (v == 11 && a.tneg && sizeof(T) == 4) v = 6;  // the fp32 LDS-DMA kernel has no -C^T epilogue
   if (v == 11) {  // LDS-DMA fp64 kernel; other dtypes / layouts / alignments take the next best tile
@@ -1127,7 +1133,7 @@ static void launch(const GemmArgs& a, hipStream_t s) {
     if constexpr (sizeof(T) == 4 && AL == 1 && MODE != MODE_RESID) {
       if (glds32_ok(a)) return launch_glds32<MODE>(a, s);
     }
-    v = sizeof(T) == 8 ? 9 : 6;
+    v = fallback;
   }
   switch (v) {
     case 1: return launch_cfg<T, AL, MODE, CfgNarrow>(a, s);

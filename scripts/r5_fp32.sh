@@ -32,3 +32,17 @@ for dn in 1 0; do
   GJ_DENSE_GEMM=$dn timeout -k 10 300 python bench/bench_emulate.py --ranks 8 --size 32768 --depth 0 --bw 50 --bcast direct --reps 1 > $o/emu_$dn.txt 2>&1 || exit $?
   echo "== p=8 N=32768 dense=$dn"; grep -h '"p"' $o/emu_$dn.txt | cut -c1-200
 done
+# every non-latency GEMM on the LDS-DMA kernel (the COMM normalisations and the look-ahead update
+# too), against the shape rule
+for rep in 1 2; do
+  for n in 8192 16384; do
+    for v in auto glds; do
+      GJ_GEMM_VARIANT=$v timeout -k 10 200 python bench.py --size $n --steps 10 --warmup 2 --no-residual > $o/b.json 2>&1 || exit $?
+      python3 -c "import json; d=json.loads(open('$o/b.json').read().splitlines()[-1]); print('n=$n variant=$v', d['ms_per_step'])"
+    done
+  done
+done
+for v in auto glds; do
+  GJ_GEMM_VARIANT=$v timeout -k 10 200 python bench.py --steps 3 --warmup 1 --no-residual > $o/b.json 2>&1 || exit $?
+  python3 -c "import json; d=json.loads(open('$o/b.json').read().splitlines()[-1]); print('n=32768 variant=$v', d['ms_per_step'])"
+done
