@@ -183,7 +183,9 @@ struct CostModel {
   double bw_gbs = 0;     // broadcast / point-to-point algorithm bandwidth, GB/s (0 = free comm)
   double lat_us = 0;     // per-collective latency (launch + handshake), us
   int channels = 16;     // workgroups a collective holds while it runs
-  int lds_kib = 32;      // LDS per channel workgroup
+  // LDS per channel workgroup: rcclGenericKernel<2, false> of a p = 2 solve declares 19 744 B
+  // (256 threads, 140 VGPRs, which the spin kernel reproduces; profiles/rccl_footprint_r5.md)
+  int lds_kib = 20;
   // The direct broadcast (Comm::bcast_direct: root -> 1/(p-1) slices over p-1 links, then the
   // slice exchange) is modelled as its two point-to-point rounds, each costing lat_us plus the
   // busiest link's bytes / bw_gbs (every peer pair has its own xGMI link).  Off: ring only.

@@ -480,6 +480,11 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, double* lds_wave
 
 // s_waitcnt vmcnt(P * n) for a runtime n <= 3: the pieces of the n most recent slices may stay in
 // flight (P pieces per slice)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 // f(std::integral_constant<int, I>) for I = B .. E-1, unrolled at compile time
 template <int B, int E, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -688,9 +693,7 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
             for (int j = 0; j < NJ; ++j) acc[i][j] = MF::op(a[i], b[j], acc[i][j]);
         }
         // slice kt + S0 + 1 landed; the NS - 2 newest may stay in flight
-        static_assert(NS == 2 || (NS == 3 && PIECES == 3), "constant waits written for 2 / 3 stages, BK 8");
-        if constexpr (NS == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        wait_vm<PIECES * (NS - 2)>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
       });
@@ -755,13 +758,15 @@ static int glds_build_forced() {
   if (g_glds_build < 0) {
     const char* e = getenv("GJ_GLDS_BUILD");
     const std::string v = e ? e : "";
-    g_glds_build = v.empty() ? 0 : v == "2.5" ? 25 : v == "3.3" ? 33 : v == "2.3" ? 23 : -2;
-    if (g_glds_build == -2) throw std::invalid_argument("GJ_GLDS_BUILD: 2.3 | 2.5 | 3.3");
+    g_glds_build = v.empty() ? 0 : v == "2.5" ? 25 : v == "3.3" ? 33 : v == "2.3" ? 23 : v == "4.3" ? 43
+                                                  : v == "16.2.3" ? 1623 : -2;
+    if (g_glds_build == -2) throw std::invalid_argument("GJ_GLDS_BUILD: 2.3 | 2.5 | 3.3 | 4.3 | 16.2.3");
   }
   return g_glds_build;
 }
 void set_glds_build(int b) {
-  if (b != 0 && b != 23 && b != 25 && b != 33) throw std::invalid_argument("glds build: 0 | 23 | 25 | 33");
+  if (b != 0 && b != 23 && b != 25 && b != 33 && b != 43 && b != 1623)
+    throw std::invalid_argument("glds build: 0 | 23 | 25 | 33 | 43 | 1623");
   g_glds_build = b;
 }
 
@@ -793,6 +798,10 @@ static void launch_glds(const GemmArgs& a0, hipStream_t s) {
       hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 5, 8, 1>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
     else if (build == 33)
       hipLaunchKernelGGL((gemm_glds_f64<MODE, 3, 3, 8, 1>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
+    else if (build == 43)  // 4 stages (53 KiB): 3 per CU
+      hipLaunchKernelGGL((gemm_glds_f64<MODE, 4, 3, 8, 1>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
+    else if (build == 1623)  // 16-deep slices, 2 stages (53 KiB): 3 per CU
+      hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 3, 16, 1>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
     else
       hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 3, 8, 1>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
   } else if (build == 25)
@@ -823,11 +832,6 @@ namespace glds32 {
 constexpr int BM = 128, BN = 128, NT = 256;
 }
 
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 __device__ __forceinline__ void dma16f(__amdgpu_buffer_rsrc_t r, float* lds_wave_base, int voff, int soff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, soff,
                                            0, 0);

@@ -152,11 +152,22 @@ __global__ __launch_bounds__(256) void spin_kernel(uint64_t ticks) {
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(4);
 }
 
+// An RCCL channel workgroup's footprint for the communication-cost model (ShadowComm): 256 threads,
+// 140 VGPRs per wave (the v139 clobber makes the allocation), the LDS passed at launch -- measured on
+// rcclGenericKernel<2, false> of a p = 2 solve (profiles/rccl_footprint_r5.md).
+__global__ __launch_bounds__(256) void spin_channel_kernel(uint64_t ticks) {
+  asm volatile("v_mov_b32 v139, 0" ::: "v139");
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(4);
+}
+
 void spin(int nwg, double us, hipStream_t s, int lds_bytes) {
   if (nwg <= 0 || !(us > 0)) return;
   const uint64_t ticks = (uint64_t)(us * 100.0);  // wall_clock64: 100 MHz
-  const unsigned nt = lds_bytes > 0 ? 256u : 64u;
-  hipLaunchKernelGGL(spin_kernel, dim3((unsigned)nwg), dim3(nt), (size_t)(lds_bytes > 0 ? lds_bytes : 0), s, ticks);
+  if (lds_bytes > 0)
+    hipLaunchKernelGGL(spin_channel_kernel, dim3((unsigned)nwg), dim3(256), (size_t)lds_bytes, s, ticks);
+  else
+    hipLaunchKernelGGL(spin_kernel, dim3((unsigned)nwg), dim3(64), 0, s, ticks);
 }
 
 template <typename T>

@@ -364,7 +364,7 @@ PYBIND11_MODULE(_C, mod) {
             return std::shared_ptr<Comm>(new ShadowComm(p, cm));
           },
           py::arg("p"), py::arg("bw_gbs") = 0.0, py::arg("lat_us") = 0.0, py::arg("channels") = 16,
-          py::arg("lds_kib") = 32, py::arg("direct") = false,
+          py::arg("lds_kib") = 20, py::arg("direct") = false,
           "rank 0 of a p-rank job alone on one device (critical-path timing emulation); bw_gbs > 0 "
           "adds the communication-cost model (lat_us + bytes/bw on `channels` spin workgroups)");
   mod.def("shadow_reset", [](std::shared_ptr<Comm> c) {
