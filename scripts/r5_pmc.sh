@@ -1,8 +1,8 @@
 #!/bin/bash
 # Round-5 evidence: (1) stall / MFMA-busy counters of the peeled 3-stage trailing-update GEMM vs the
 # round-4 kernel vs hipBLASLt at 32768 x 8192 x 512 (one --pmc pass per run, per-block limits kept,
-# no trace domains combined); (2) N = 32768 kernel trace; (3) RCCL kernels' CU footprint (p = 2
-# --same-gpu rehearsal).
+# no trace domains combined); (2) N = 32768 kernel trace.  The RCCL footprint and the deeper-pipeline
+# A/B run in scripts/r5_next.sh.
 cd "$(dirname "$0")/.." || exit 1
 export TMPDIR=/tmp
 out=gpurun_out/pmc5
@@ -29,15 +29,3 @@ python3 scripts/pmc_table.py "$out" > "$out/table.md"
 cat "$out/table.md"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/prof32k -o run -- python3 bench.py --steps 2 --warmup 1 --no-residual > $out/prof32k.log 2>&1
 echo "trace rc=$?"
-bash scripts/r5_rcclfp.sh
-# deeper pipelines of the peeled loop: 4 stages or 16-deep slices (both 3 per CU) vs 3.3
-for b in 3.3 4.3 16.2.3; do
-  GJ_GLDS_BUILD=$b timeout -k 10 120 python bench/gemm_probe.py 32768 8192 512 --ldc 32768 --reps 30 > $out/g.json 2>&1 || exit $?
-  echo "gemm alone build=$b $(tail -1 $out/g.json | cut -c150-220)"
-done
-for rep in 1 2; do
-  for b in 3.3 4.3 16.2.3; do
-    GJ_GLDS_BUILD=$b timeout -k 10 200 python bench.py --steps 3 --warmup 1 --no-residual > $out/b.json 2>&1 || exit $?
-    python3 -c "import json; d=json.loads(open('$out/b.json').read().splitlines()[-1]); print('n=32768 build=$b', d['ms_per_step'])"
-  done
-done
