@@ -200,7 +200,8 @@ class Engine {
     bool la_side = true;          // look-ahead rows on SIDE (else COMM)
     std::string pivot;            // "block-min-inv-norm" | "partial"
     std::string fault_injection;  // active GJ_TEST_* knobs ("" in every normal run)
-    bool split = false;           // chain / deferred split of the column updates (split_)
+    int split = 0;                // chain / deferred split of the column updates (split_: 0, 1, 2)
+    bool lat_wide = false;        // chain column updates on the LDS-DMA kernel (lat_wide_)
   };
   Policy policy() const;
   const std::string& bcast_algo() const { return bcast_algo_; }  // "ring" | "direct"
@@ -288,17 +289,20 @@ class Engine {
   int reserved_cus_ = 0;
   bool dense_gemm_ = false;        // trailing update at 5 workgroups per CU (GemmExtra::dense)
   bool la_side_ = true;            // look-ahead rows on SIDE (else COMM); GJ_LA_SIDE overrides
-  // Chain / deferred split of a panel's column updates (opt-in, GJ_SPLIT=1; measured slower by
-  // default, profiles/split_r5.md): the look-ahead
-  // update and the in-panel column updates on the pivot chain (SIDE) cover only the local block rows
-  // that are still pivot candidates when the panel starts (chain_sel_); the rows already used as
-  // pivot rows (defer_sel_) get the same updates later, on COMM ahead of the panel's chunk pass --
-  // they are needed only by MAIN's trailing update.  Bit-identical results (same products, same k
-  // order per row).  Needs 64 | m and <= 512 local blocks (GemmExtra::rsel).
-  bool split_ = false;
+  // Chain / deferred split of a panel's column updates (GJ_SPLIT, profiles/split_r5.md): the
+  // look-ahead update and the in-panel column updates on the pivot chain (SIDE) cover only the local
+  // block rows that are still pivot candidates when the panel starts (chain_sel_); the rows already
+  // used as pivot rows (defer_sel_) get the same updates later -- they are needed only by MAIN's
+  // trailing update: 1 = on COMM ahead of the panel's chunk pass, 2 = on MAIN ahead of the panel's
+  // trailing update.  Bit-identical results (same products, same k order per row).  Needs 64 | m
+  // and <= 512 local blocks (GemmExtra::rsel).
+  int split_ = 0;
+  // the pivot chain's column updates (rows x m x j m) on the LDS-DMA kernel instead of the 64 x 32
+  // latency tile (GemmExtra::lat_wide): on when CUs are reserved for the chain at p = 1
+  bool lat_wide_ = false;
   std::vector<char> used_local_;       // local blocks used as pivot rows so far (host copy)
   GemmExtra chain_sel_[2], defer_sel_[2];  // by panel parity; rsel_m == 0: panel without a split
-  void deferred_updates(int64_t v);
+  void deferred_updates(int64_t v, int stream);
   double norm_a_ = -1;
 
   // chunk plan (block-column ranges, multiples of d_ blocks so a panel never straddles chunks)
@@ -357,6 +361,7 @@ class Engine {
   int ev_pp_[2][kMaxDepth] = {};
   int ev_la_[2] = {-1, -1};            // LA_[par] formed and broadcast (COMM)
   int ev_cp_[2] = {-1, -1};            // chunk pass of a panel of that parity done (COMM)
+  int ev_def_[2] = {-1, -1};           // split_ == 2: MAIN's deferred updates of that panel done
   std::vector<int> ev_c_;        // per chunk: MAIN finished the panel update of that chunk
   std::vector<int> ev_b_[2];     // per chunk: all stacked rows of that chunk broadcast
   std::vector<int> pev_pool_;    // profiling events (timing enabled), reused across solves

@@ -142,6 +142,7 @@ struct GemmArgs {
   double* partial;  // [M][nparts]
   int nparts;
   bool latency;     // GemmExtra::latency -> CfgSmall for few-tile launches
+  bool lat_wide;    // GemmExtra::lat_wide
   int group;        // LDS-DMA kernel: tile rows per column-walk group (1 = row-major tile order)
   void* tneg;       // GemmExtra::tneg: -C^T of the columns < tncols also written here
   int64_t ldt, tncols;
@@ -536,7 +537,9 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
   const int gsz = (g.tiles_m - gr0) < G ? (g.tiles_m - gr0) : G;
   const int rem = tile - grp * G * g.tiles_n;
   const int tm = gr0 + rem % gsz, tn = rem / gsz;
-  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  // m0L logical / m0 physical first row (GemmExtra::rsel, as in gemm_tile)
+  const int64_t m0L = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t m0 = g.rsel_m > 0 ? rsel_map(g, m0L) : m0L;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
@@ -547,7 +550,7 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
 
   const int rlane = wm * TM + MF::rl(lane);
   const int clane = wn * TN + (lane & 15);
-  const int Mt = (int)((g.M - m0) < BM ? (g.M - m0) : BM);
+  const int Mt = (int)((g.M - m0L) < BM ? (g.M - m0L) : BM);
   const int Nt = (int)((g.N - n0) < BN ? (g.N - n0) : BN);
   const int64_t zlo = g.zc0 - n0, zhi = g.zc1 - n0;
   const int z0 = (int)(zlo < 0 ? 0 : (zlo > BN ? BN : zlo)), z1 = (int)(zhi < 0 ? 0 : (zhi > BN ? BN : zhi));
@@ -593,7 +596,7 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
   // DMA piece geometry (per wave, per slice): A rows wid and wid + 4 (lane l -> columns 2l, 2l+1);
   // B rows 2 wid + (l >> 5), columns 2 (l & 31) of the swizzled image.
   const int acol = 2 * lane;
-  const bool a_ok = (m0 + acol) < g.M;
+  const bool a_ok = (m0L + acol) < g.M;
   const int brow = 2 * wid + (lane >> 5);
   const int bpos = 2 * (lane & 31);
   const int bcol = bpos ^ ((brow & 1) * 16);
@@ -864,7 +867,9 @@ __global__ __launch_bounds__(glds32::NT, OCC) void gemm_glds_f32(GemmArgs g) {
   const int gsz = (g.tiles_m - gr0) < G ? (g.tiles_m - gr0) : G;
   const int rem = tile - grp * G * g.tiles_n;
   const int tm = gr0 + rem % gsz, tn = rem / gsz;
-  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  // m0L logical / m0 physical first row (GemmExtra::rsel, as in gemm_tile)
+  const int64_t m0L = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int64_t m0 = g.rsel_m > 0 ? rsel_map(g, m0L) : m0L;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
@@ -875,7 +880,7 @@ __global__ __launch_bounds__(glds32::NT, OCC) void gemm_glds_f32(GemmArgs g) {
 
   const int rlane = wm * TM + 4 * (lane >> 5);
   const int clane = wn * TN + (lane & 31);
-  const int Mt = (int)((g.M - m0) < BM ? (g.M - m0) : BM);
+  const int Mt = (int)((g.M - m0L) < BM ? (g.M - m0L) : BM);
   const int Nt = (int)((g.N - n0) < BN ? (g.N - n0) : BN);
   const int64_t zlo = g.zc0 - n0, zhi = g.zc1 - n0;
   const int z0 = (int)(zlo < 0 ? 0 : (zlo > BN ? BN : zlo)), z1 = (int)(zhi < 0 ? 0 : (zhi > BN ? BN : zhi));
@@ -920,7 +925,7 @@ __global__ __launch_bounds__(glds32::NT, OCC) void gemm_glds_f32(GemmArgs g) {
 
   // DMA piece (per wave): k rows 2 (wid + 4h) + (lane >> 5), floats 4 (lane & 31) .. + 3
   const int dcol = 4 * (lane & 31), drow = lane >> 5;
-  const bool a_ok = (m0 + dcol) < g.M, b_ok = (n0 + dcol) < g.N;
+  const bool a_ok = (m0L + dcol) < g.M, b_ok = (n0 + dcol) < g.N;
   __amdgpu_buffer_rsrc_t ra = rsrc(A + m0);
   __amdgpu_buffer_rsrc_t rb = rsrc(B + n0);
   const int Kd = (int)g.K;
@@ -1100,17 +1105,49 @@ void set_gemm_variant(int v) { g_variant = v; }
 // (the panel-factorisation GEMMs: m x m .. m x d*m outputs, or rows x m column updates).
 constexpr int64_t kSmallGridTiles = 512;
 
+// GemmExtra::lat_wide (or set_lat_glds() for every launch, tests): latency launches of >=
+// kLatGldsRows rows (the pivot chain's column updates: rows x m x j m) on the LDS-DMA kernel
+// (128 x 64 tiles, 4 per CU) instead of the 64 x 32 register-staged latency tile
+constexpr int64_t kLatGldsRows = 1024;
+static int g_lat_glds = 0;
+static bool lat_glds(const GemmArgs& a) { return a.lat_wide || g_lat_glds; }
+void set_lat_glds(int on) { g_lat_glds = on ? 1 : 0; }
+
+// the LDS-DMA kernel of T when it takes the shape (K-major A, no C_in; fp32: no -C^T epilogue)
+template <typename T, int AL, int MODE>
+static bool try_glds(const GemmArgs& a, hipStream_t s) {
+  if constexpr (AL == 1 && MODE != MODE_RESID) {
+    if (a.cin) return false;
+    if constexpr (sizeof(T) == 8) {
+      if (glds_ok(a)) {
+        launch_glds<MODE>(a, s);
+        return true;
+      }
+    } else {
+      if (!a.tneg && glds32_ok(a)) {
+        launch_glds32<MODE>(a, s);
+        return true;
+      }
+    }
+  }
+  return false;
+}
+
 template <typename T, int AL, int MODE>
 static void launch(const GemmArgs& a, hipStream_t s) {
   if (MODE == MODE_RESID) return launch_cfg<T, AL, MODE, CfgBig>(a, s);
-  if (a.rsel_m > 0) {  // row-block selection: register-staged tiles whose height divides the block
+  if (a.rsel_m > 0) {  // row-block selection: LDS-DMA (128-row tiles) or register-staged tiles whose height divides the block
+    const bool v_glds = gemm_variant() == kAutoVariant || gemm_variant() == 11;
+    if (a.rsel_m % 128 == 0 && v_glds && (!a.latency || lat_glds(a)) && try_glds<T, AL, MODE>(a, s)) return;
     if (a.rsel_m % CfgNarrow::BM == 0 && !a.latency) return launch_cfg<T, AL, MODE, CfgNarrow>(a, s);
     if (a.rsel_m % CfgSmall::BM == 0) return launch_cfg<T, AL, MODE, CfgSmall>(a, s);
     throw Error(Status::BadArgs, "gemm: a row-block selection needs 64 | block height");
   }
   const int64_t narrow_tiles = ((a.M + CfgNarrow::BM - 1) / CfgNarrow::BM) * ((a.N + CfgNarrow::BN - 1) / CfgNarrow::BN);
-  if (a.latency && narrow_tiles < kSmallGridTiles && gemm_variant() != 0)
+  if (a.latency && narrow_tiles < kSmallGridTiles && gemm_variant() != 0) {
+    if (lat_glds(a) && a.M >= kLatGldsRows && gemm_variant() == kAutoVariant && try_glds<T, AL, MODE>(a, s)) return;
     return launch_cfg<T, AL, MODE, CfgSmall>(a, s);
+  }
   if (a.cin) return launch_cfg<T, AL, MODE, CfgNarrow>(a, s);  // C_in: register-staged tiles only
   int v = gemm_variant();
   int fallback = sizeof(T) == 8 ? 9 : 6;  // when the LDS-DMA kernel cannot take the shape
@@ -1154,6 +1191,7 @@ static void fill_extra(GemmArgs& a, const GemmExtra* ex) {
   a.zh = ex ? ex->zh : 0;
   for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) a.zr[z] = (ex && z < ex->nzr) ? ex->zr[z] : kNone;
   a.latency = ex ? ex->latency : false;
+  a.lat_wide = ex ? ex->lat_wide : false;
   a.tneg = ex ? ex->tneg : nullptr;
   a.ldt = ex ? ex->ldtneg : 0;
   a.tncols = (ex && ex->tneg_cols > 0) ? ex->tneg_cols : (int64_t(1) << 62);

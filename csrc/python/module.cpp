@@ -177,7 +177,9 @@ PYBIND11_MODULE(_C, mod) {
   mod.def("set_glds_peel", [](bool on) { kern::set_glds_peel(on ? 1 : 0); },
           "fp64 LDS-DMA trailing-update kernel: the peeled, stage-unrolled main loop (GJ_GLDS_PEEL)");
   mod.def("set_glds_build", [](int b) { kern::set_glds_build(b); },
-          "fp64 LDS-DMA trailing-update build for every launch: 23 | 25 | 33, 0 = auto (GJ_GLDS_BUILD)");
+          "fp64 LDS-DMA trailing-update build for every launch: 23 | 25 | 33 | 43 | 1623, 0 = auto (GJ_GLDS_BUILD)");
+  mod.def("set_lat_glds", [](bool on) { kern::set_lat_glds(on ? 1 : 0); },
+          "every latency GEMM of >= 1024 rows on the LDS-DMA kernel (tests; the engine sets it per launch)");
 
   // Kernel-level entry points (raw pointers; used by the per-kernel numerics tests and
   // mpi_jordan_crazy_acceleration_amd.ops).  Every op runs on the MAIN stream and is waited for.
@@ -467,6 +469,7 @@ PYBIND11_MODULE(_C, mod) {
                                d["pivot"] = pl.pivot;
                                if (!pl.fault_injection.empty()) d["fault_injection"] = pl.fault_injection;
                                d["split"] = pl.split;
+                               d["lat_wide"] = pl.lat_wide;
                                d["bcast"] = e.eng->bcast_algo();
                                d["bcast_tuning"] = e.comm->bcast_report();
                                d["comm"] = e.comm->describe();

@@ -224,14 +224,23 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   if (const char* e = std::getenv("GJ_LA_SIDE")) la_side_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("GJ_HOST_FREE")) host_free_multi_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("GJ_COMM_SMALL_TILES")) comm_small_tiles_ = std::atoi(e) != 0;
-  // Measured round 5 (scripts/r5_ab.sh, one box, two repetitions): N = 8192 25.35 / 25.49 ->
-  // 25.90 / 25.96 ms, N = 16384 159.6 / 160.7 -> 158.9 / 158.5, N = 32768 1130 / 1131 -> 1139 /
-  // 1139 ms, emulated p = 4 at N = 16384 (direct 50 GB/s) 0.0515 -> 0.0586 s: the deferred half
-  // delays COMM's chunk pass and runs on the same reserved CUs as the chain.  Off by default;
-  // GJ_SPLIT=1 turns it on (profiles/split_r5.md).
-  split_ = false;
-  if (const char* e = std::getenv("GJ_SPLIT"))
-    split_ = std::atoi(e) != 0 && L_.m % 64 == 0 && L_.nblk <= 64 * GemmExtra::kRselWords && L_.nblk > 0;
+  // Measured round 5 (scripts/r5_ab.sh, one box, two repetitions), deferred half on COMM (1):
+  // N = 8192 25.35 / 25.49 -> 25.90 / 25.96 ms, N = 16384 159.6 / 160.7 -> 158.9 / 158.5, N = 32768
+  // 1130 / 1131 -> 1139 / 1139 ms, emulated p = 4 at N = 16384 (direct 50 GB/s) 0.0515 -> 0.0586 s:
+  // it delays COMM's chunk pass and runs on the same reserved CUs as the chain.  GJ_SPLIT=2 puts it
+  // on MAIN instead (profiles/split_r5.md).
+  // Chain column updates on the LDS-DMA kernel where the chain has reserved CUs at p = 1
+  // (scripts/r5_split2.sh / r5_latglds.sh, one box, two repetitions): N = 8192 24.58 / 24.55 ->
+  // 24.38 / 24.34 ms, N = 16384 152.2 / 152.0 -> 152.4 / 152.1; without a reservation (N = 32768)
+  // 1100.1 / 1100.2 -> 1105.6 / 1101.4 ms, emulated p = 4 / 8 even.  GJ_LAT_GLDS=0/1 overrides.
+  lat_wide_ = reserved_cus_ > 0 && L_.p == 1;
+  if (const char* e = std::getenv("GJ_LAT_GLDS")) lat_wide_ = std::atoi(e) != 0;
+  split_ = 0;
+  if (const char* e = std::getenv("GJ_SPLIT")) {
+    const int v = std::atoi(e);
+    if (v < 0 || v > 2) throw Error(Status::BadArgs, "GJ_SPLIT: 0 | 1 | 2");
+    if (L_.m % 64 == 0 && L_.nblk <= 64 * GemmExtra::kRselWords && L_.nblk > 0) split_ = v;
+  }
 
 }
 
@@ -254,6 +263,7 @@ Engine::Policy Engine::policy() const {
   p.pivot = opt_.pivot == PivotRule::Partial ? "partial" : "block-min-inv-norm";
   p.fault_injection = fault_injection_;
   p.split = split_;
+  p.lat_wide = lat_wide_;
   return p;
 }
 
@@ -370,6 +380,7 @@ void Engine::alloc_work(int64_t wmax) {
     for (int j = 0; j < kMaxDepth; ++j) ev_pp_[i][j] = dev_.create_event();
     ev_la_[i] = dev_.create_event();
     ev_cp_[i] = dev_.create_event();
+    ev_def_[i] = dev_.create_event();
     for (size_t c = 0; c < cb0_.size(); ++c) ev_b_[i].push_back(dev_.create_event());
   }
   for (size_t c = 0; c < cb0_.size(); ++c) ev_c_.push_back(dev_.create_event());
@@ -744,6 +755,7 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
         // (split_: the rows still candidates at the panel's start; the others in deferred_updates)
         GemmExtra ex = chain_sel_[par];
         ex.latency = true;
+        ex.lat_wide = lat_wide_;
         ex.tneg = Lt;
         ex.ldtneg = rows;
         const int64_t M = ex.rsel_m > 0 ? ex.rsel_count() * m : rows;
@@ -973,7 +985,7 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
   if (vparts_)  // the last step's piece: no column update consumes it, the chunk pass does first
     vhash(v, vslot(V_PP, q - 1), elem(PP_[par], (q - 1) * m * (int64_t)d_ * m), (int64_t)d_ * m * (int64_t)es,
           (int64_t)d_ * m * (int64_t)es, m, S_COMM);
-  deferred_updates(v);
+  if (split_ == 1) deferred_updates(v, S_COMM);
   cur_phase_ = "pivot-row broadcast";
   for (int64_t i = 0; i < C; ++i) {
     const int64_t c = (start + i) % C;
@@ -1058,10 +1070,11 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
 
 // The split_ half that left the pivot chain: for the rows already used as pivot rows when panel v
 // started, panel v-1's look-ahead update of panel v's columns (with its -X^T segment 0 of At) and
-// panel v's in-panel column updates (segments 1..q-1), on COMM right after the last panel piece and
-// ahead of the panel's chunk pass (so ahead of MAIN's trailing update, the only reader of these
-// rows' multipliers).  The products and their k order are the chain's, row for row.
-void Engine::deferred_updates(int64_t v) {
+// panel v's in-panel column updates (segments 1..q-1), after the last panel piece: on COMM ahead of
+// the panel's chunk pass (split_ 1) or on MAIN ahead of the panel's trailing update (split_ 2), in
+// either case ahead of MAIN's trailing update, the only reader of these rows' multipliers.  The
+// products and their k order are the chain's, row for row.
+void Engine::deferred_updates(int64_t v, int stream) {
   const int par = (int)(v & 1);
   const GemmExtra& sel = defer_sel_[par];
   if (v == 0 || sel.rsel_m == 0 || L_.rows == 0) return;
@@ -1070,7 +1083,7 @@ void Engine::deferred_updates(int64_t v) {
   const int64_t m = L_.m, rows = L_.rows, npad = L_.npad, dm = (int64_t)d_ * m, M = cnt * m;
   const int64_t q = panel_q(v), x0 = panel_t0(v) * m, qp = panel_q(v - 1);
   cur_phase_ = "deferred column updates";
-  const int pe = prof_begin(S_COMM);
+  const int pe = prof_begin(stream);
   GemmExtra ex = pivot_rows_extra((int)((v - 1) & 1), qp);
   std::copy(sel.rsel, sel.rsel + GemmExtra::kRselWords, ex.rsel);
   ex.rsel_m = sel.rsel_m;
@@ -1078,16 +1091,17 @@ void Engine::deferred_updates(int64_t v) {
   ex.ldtneg = rows;
   ex.tneg_cols = m;
   dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, M, q * m, qp * m, At_[(v - 1) % 3], rows,
-            LA_[(v - 1) & 1], q * m, elem(X_, x0), npad, S_COMM, ex);
+            LA_[(v - 1) & 1], q * m, elem(X_, x0), npad, stream, ex);
   for (int64_t j = 1; j < q; ++j) {
     GemmExtra ec = sel;
     ec.latency = true;
+    ec.lat_wide = lat_wide_;
     ec.tneg = elem(At_[v % 3], j * m * rows);
     ec.ldtneg = rows;
     dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, M, m, j * m, At_[v % 3], rows, elem(PP_[par], j * m), dm,
-              elem(X_, x0 + j * m), npad, S_COMM, ec);
+              elem(X_, x0 + j * m), npad, stream, ec);
   }
-  prof_end(PH_COLUMN, pe, S_COMM);
+  prof_end(PH_COLUMN, pe, stream);
 }
 
 // First part of panel u's depth-q trailing update: the next panel's block columns (look-ahead), so
@@ -1109,13 +1123,17 @@ void Engine::lookahead_update(int64_t u) {
     const int64_t tn = panel_t0(u + 1), qn = panel_q(u + 1);
     const int ms = S_SIDE;
     const int64_t x0 = tn * m, x1 = (tn + qn) * m;
+    // split_ 2: MAIN's deferred updates of panel u-1 read At_[(u-1) % 3], LA_ / PP_ of parity u-1
+    // and write X and At_ rows that SIDE rewrites from here on (normally implied by the look-ahead
+    // rows' wait for MAIN's chunk; explicit here)
+    if (split_ == 2 && u >= 1) dev_.wait(ms, ev_def_[(u - 1) & 1]);
     const GemmExtra prows = pivot_rows_extra(par, q);
     // the look-ahead rows of panel u (lookahead_rows): N = 16384 emulated p = 4 / 8 at 50 GB/s per
     // link 0.0669 -> 0.0595 s / 0.0485 -> 0.0431 s against waiting for the whole first chunk
     // (profiles/emu_direct_r3.md)
     // split_: this update and the next panel's column updates cover the rows still candidates
     // when panel u+1 starts (every pivot of panel u is known on the host by now); the rows used
-    // before get both in deferred_updates(u + 1) on COMM
+    // before get both in deferred_updates(u + 1) (COMM or MAIN)
     const int npar = (int)((u + 1) & 1);
     chain_sel_[npar] = GemmExtra{};
     defer_sel_[npar] = GemmExtra{};
@@ -1166,6 +1184,11 @@ void Engine::big_update(int64_t u) {
   const int64_t x1 = has_next ? (panel_t0(u + 1) + panel_q(u + 1)) * m : -1;
   const int64_t start = has_next ? chunk_of_[panel_t0(u + 1)] : 0;
   const int64_t pc0 = t0 * m, pc1 = (t0 + q) * m;
+  if (split_ == 2) {  // the used rows' column updates, behind the panel's last piece (SIDE)
+    dev_.wait(S_MAIN, ev_pp_[par][q - 1]);
+    deferred_updates(u, S_MAIN);
+    dev_.record(ev_def_[par], S_MAIN);
+  }
   for (int64_t i = 0; i < C; ++i) {
     const int64_t c = (start + i) % C;
     const int64_t c0 = cb0_[c] * m, c1 = cb1_[c] * m, W = c1 - c0;

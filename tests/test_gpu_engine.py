@@ -167,18 +167,25 @@ def test_device_resident_fp32_solve_is_refined(k):
 
 
 @pytest.mark.parametrize("p,comm,depth", [(1, "auto", 2), (1, "auto", 4), (3, "async", 4), (8, "async", 2)])
-def test_split_column_updates_bit_identical_on_gpu(p, comm, depth, monkeypatch):
-    """Engine::split_ on the GPU: the chain's row-selected look-ahead / column updates (GemmExtra::rsel)
-    plus the deferred ones on COMM give the unsplit inverse bit for bit (same products, same k
-    order; the narrow tile replaces the LDS-DMA one for the look-ahead update)."""
+def test_split_column_updates_bit_identical_on_gpu(p, comm, depth, monkeypatch, native):
+    """Engine::split_ on the GPU: the chain's row-selected look-ahead / column updates (GemmExtra::rsel,
+    LDS-DMA kernel for 128-row blocks) plus the deferred ones on COMM (1) or MAIN (2) give the
+    unsplit inverse bit for bit (same products, same k order), with the chain's column updates on
+    the latency tile or the LDS-DMA kernel (GJ_LAT_GLDS)."""
     n, m = 2560, 128
     A = generate_matrix(n, "random", 21)[::-1].copy()
     out = []
-    for split in ("0", "1"):
+    for split, lat in (("0", "0"), ("1", "0"), ("2", "0"), ("0", "1"), ("2", "1")):
         monkeypatch.setenv("GJ_SPLIT", split)
-        out.append(gj.GaussJordan(block_size=m, ranks=p, device="gpu", comm=comm, depth=depth,
-                                  jitter_us=30.0 if comm == "async" else 0.0).inverse(A))
-    assert np.array_equal(out[0], out[1])
+        monkeypatch.setenv("GJ_LAT_GLDS", lat)  # the engine's choice (GemmExtra::lat_wide) ...
+        native.set_lat_glds(lat == "1")         # ... and every other latency launch
+        try:
+            out.append(gj.GaussJordan(block_size=m, ranks=p, device="gpu", comm=comm, depth=depth,
+                                      jitter_us=30.0 if comm == "async" else 0.0).inverse(A))
+        finally:
+            native.set_lat_glds(False)
+    for o in out[1:]:
+        assert np.array_equal(out[0], o)
     assert np.abs(out[1] - np.linalg.inv(A)).max() / np.abs(out[1]).max() < 1e-8
 
 

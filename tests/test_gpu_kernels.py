@@ -157,14 +157,23 @@ def test_block_inverse_large_m_panel_blocked(native, m, dtype):
 
 
 @pytest.mark.parametrize("m,blocks,latency", [(64, [0, 2, 3, 7], True), (128, [1, 4], False), (128, [0], True),
-                                              (64, list(range(8)), False)])
+                                              (64, list(range(8)), False), (128, [0, 3, 5, 6, 7], True)])
 @pytest.mark.parametrize("c_in", [False, True])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
-def test_gemm_row_blocks_and_c_in(m, blocks, latency, c_in, dtype):
+@pytest.mark.parametrize("lat_glds", [False, True])
+def test_gemm_row_blocks_and_c_in(m, blocks, latency, c_in, dtype, lat_glds, native):
     """GemmExtra::rsel (the split pivot chain's row-selected column updates) and GemmExtra::c_in (the
     owners' normalisation input without a copy): only the selected row blocks of C and -C^T change,
     with C_in + A B; the others keep their bytes.  Same k order as the full product: bit-identical
-    rows."""
+    rows.  128-row blocks take the LDS-DMA kernel (latency launches too with set_lat_glds)."""
+    native.set_lat_glds(lat_glds)
+    try:
+        _row_blocks_case(m, blocks, latency, c_in, dtype)
+    finally:
+        native.set_lat_glds(False)
+
+
+def _row_blocks_case(m, blocks, latency, c_in, dtype):
     M, N, K = 8 * m, 192, 3 * m
     A = _rand((M, K), torch.float64, 41).to(dtype).cuda()
     B = _rand((K, N), torch.float64, 42).to(dtype).cuda()

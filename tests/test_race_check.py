@@ -159,3 +159,15 @@ def test_look_ahead_rows_on_comm_race_free(p, depth, monkeypatch):
     rep = _run(420, 20, p, depth=depth, chunk_cols=120)
     assert rep["race_count"] == 0, "\n".join(rep["races"])
     assert rep["residual"] < 1e-8
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("p,depth,la_side", [(1, 2, "1"), (1, 4, "1"), (3, 2, "1"), (8, 2, "1"), (3, 4, "0")])
+def test_split_column_updates_race_free(mode, p, depth, la_side, monkeypatch):
+    """GJ_SPLIT=1/2 (the used rows' column updates deferred to COMM / MAIN): every deferred product
+    is ordered against the chain's and the trailing update's accesses of the same rows."""
+    monkeypatch.setenv("GJ_SPLIT", str(mode))
+    monkeypatch.setenv("GJ_LA_SIDE", la_side)
+    rep = _run(64 * 11, 64, p, depth=depth, chunk_cols=64 * 3, jitter_us=20.0)
+    assert rep["race_count"] == 0, "\n".join(rep["races"])
+    assert rep["residual"] < 1e-8

@@ -79,7 +79,7 @@ def test_verify_flag_on_the_cli_and_clean_exit():
 
 # ---------------------------------------------------------------- chain / deferred split (Engine::split_)
 def _inv_split(split, n, m, p, depth, comm="async", jitter=200.0, monkeypatch=None, **extra):
-    monkeypatch.setenv("GJ_SPLIT", "1" if split else "0")
+    monkeypatch.setenv("GJ_SPLIT", str(int(split)))
     eng = gj.GaussJordan(block_size=m, ranks=p, device="cpu", comm=comm, depth=depth, jitter_us=jitter,
                          host_threads=2, extra=dict(verify=True, **extra))
     rep = eng.run(n, gen="random", seed=8, keep_inverse=True)
@@ -87,14 +87,15 @@ def _inv_split(split, n, m, p, depth, comm="async", jitter=200.0, monkeypatch=No
     return rep["inverse"]
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("p,depth", [(1, 2), (1, 4), (3, 3), (8, 2), (4, 1)])
-def test_split_column_updates_bit_identical(p, depth, monkeypatch):
+def test_split_column_updates_bit_identical(p, depth, mode, monkeypatch):
     """The look-ahead and in-panel column updates of the rows already used as pivot rows leave the
-    pivot chain (deferred to COMM): the inverse is bit-identical to the unsplit schedule, under
-    jittered asynchronous ranks with consumption-point verification on."""
+    pivot chain (deferred to COMM: mode 1, to MAIN: mode 2): the inverse is bit-identical to the
+    unsplit schedule, under jittered asynchronous ranks with consumption-point verification on."""
     n, m = 64 * 11, 64
-    a = _inv_split(False, n, m, p, depth, monkeypatch=monkeypatch)
-    b = _inv_split(True, n, m, p, depth, monkeypatch=monkeypatch)
+    a = _inv_split(0, n, m, p, depth, monkeypatch=monkeypatch)
+    b = _inv_split(mode, n, m, p, depth, monkeypatch=monkeypatch)
     assert np.array_equal(a, b)
     A = generate_matrix(n, "random", 8)
     from mpi_jordan_crazy_acceleration_amd.utils.metrics import residual_ok
@@ -102,10 +103,11 @@ def test_split_column_updates_bit_identical(p, depth, monkeypatch):
     assert residual_ok(res, n, np.abs(A).sum(1).max(), np.abs(b).sum(1).max()), res
 
 
-def test_split_with_partial_pivoting(monkeypatch):
+@pytest.mark.parametrize("mode", [1, 2])
+def test_split_with_partial_pivoting(mode, monkeypatch):
     n, m = 64 * 9, 64
-    a = _inv_split(False, n, m, 3, 3, monkeypatch=monkeypatch, pivot="partial")
-    b = _inv_split(True, n, m, 3, 3, monkeypatch=monkeypatch, pivot="partial")
+    a = _inv_split(0, n, m, 3, 3, monkeypatch=monkeypatch, pivot="partial")
+    b = _inv_split(mode, n, m, 3, 3, monkeypatch=monkeypatch, pivot="partial")
     assert np.array_equal(a, b)
 
 
@@ -113,7 +115,16 @@ def test_split_policy_reported_and_off_when_not_applicable(native, monkeypatch):
     def pol(m):
         eng = native.Engine(native.host_device(2), native.self_comm(), 600, m, "fp64")
         return eng.policy["split"]
-    assert pol(64) is False  # opt-in (measured slower by default, profiles/split_r5.md)
+    assert pol(64) == 0  # opt-in (profiles/split_r5.md)
     monkeypatch.setenv("GJ_SPLIT", "1")
-    assert pol(64) is True
-    assert pol(60) is False  # the GPU tiles need 64 | m
+    assert pol(64) == 1
+    assert pol(60) == 0  # the GPU tiles need 64 | m
+    monkeypatch.setenv("GJ_SPLIT", "2")
+    assert pol(64) == 2
+    monkeypatch.setenv("GJ_SPLIT", "3")
+    with pytest.raises(Exception, match="GJ_SPLIT"):
+        pol(64)
+    monkeypatch.setenv("GJ_SPLIT", "0")
+    assert native.Engine(native.host_device(2), native.self_comm(), 600, 64, "fp64").policy["lat_wide"] is False
+    monkeypatch.setenv("GJ_LAT_GLDS", "1")
+    assert native.Engine(native.host_device(2), native.self_comm(), 600, 64, "fp64").policy["lat_wide"] is True
