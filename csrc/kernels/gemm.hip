@@ -744,7 +744,7 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
 // GJ_GLDS_PEEL=0/1 or set_glds_peel(): the peeled, stage-unrolled main loop (PEEL template
 // argument; default on since round 5).  32768 x 8192 x 512 alone, one box: 2 stages 63.65 -> 66.56
 // TF/s, 3 stages 61.24 -> 67.57; the N = 32768 solve 1139 -> 1114 (2 stages) -> 1092-1093 ms
-// (3 stages), two repetitions (scripts/r5_ab.sh, profiles/gemm_peel_r5.md).
+// (3 stages), two repetitions (scripts/runs/r5_ab.sh, profiles/gemm_peel_r5.md).
 static int g_glds_peel = -1;
 static int glds_peel() {
   if (g_glds_peel < 0) {
@@ -1160,7 +1160,7 @@ static void launch(const GemmArgs& a, hipStream_t s) {
     // Round 5, with the peeled LDS-DMA loop: every fp64 non-latency product takes it (the owners'
     // row normalisations of the chunk pass, the look-ahead update at N <= 16384 too): N = 8192
     // 25.54 / 24.95 -> 24.65 / 24.54 ms, N = 16384 153.4 / 152.7 -> 152.8 / 152.3, N = 32768 even
-    // (scripts/r5_fp32.sh, profiles/gemm_peel_r5.md).
+    // (scripts/runs/r5_fp32.sh, profiles/gemm_peel_r5.md).
     const int64_t big_tiles = ((a.M + 127) / 128) * ((a.N + 127) / 128);
     const bool deep = a.K >= (sizeof(T) == 8 ? 256 : 384) && big_tiles >= 512;
     v = (deep || sizeof(T) == 8) ? 11 : 1;

@@ -214,7 +214,7 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // workgroups of the 128x64 tile.  Round 2 (profiles/small_n_sweep.md): N = 8192 30.2 -> 29.3 ms,
   // N = 16384 +1.1 %, N = 32768 +0.7 %.  Round 4, with the look-ahead rows on SIDE the chunk pass
   // is off the pivot chain at every size: N = 8192 25.80 / 25.74 (small) vs 25.66 / 25.56 ms,
-  // N = 16384 even (scripts/r4_cst.sh) -- off by default; GJ_COMM_SMALL_TILES=1 turns it on.
+  // N = 16384 even (scripts/runs/r4_cst.sh) -- off by default; GJ_COMM_SMALL_TILES=1 turns it on.
   comm_small_tiles_ = false;
   // Look-ahead rows on SIDE, right behind the panel pieces, at every p (GJ_LA_SIDE=0 puts them on
   // COMM at p = 1, round 3's one-rank choice): with the host-free pivot chain, COMM's queue (the
@@ -224,13 +224,13 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   if (const char* e = std::getenv("GJ_LA_SIDE")) la_side_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("GJ_HOST_FREE")) host_free_multi_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("GJ_COMM_SMALL_TILES")) comm_small_tiles_ = std::atoi(e) != 0;
-  // Measured round 5 (scripts/r5_ab.sh, one box, two repetitions), deferred half on COMM (1):
+  // Measured round 5 (scripts/runs/r5_ab.sh, one box, two repetitions), deferred half on COMM (1):
   // N = 8192 25.35 / 25.49 -> 25.90 / 25.96 ms, N = 16384 159.6 / 160.7 -> 158.9 / 158.5, N = 32768
   // 1130 / 1131 -> 1139 / 1139 ms, emulated p = 4 at N = 16384 (direct 50 GB/s) 0.0515 -> 0.0586 s:
   // it delays COMM's chunk pass and runs on the same reserved CUs as the chain.  GJ_SPLIT=2 puts it
   // on MAIN instead (profiles/split_r5.md).
   // Chain column updates on the LDS-DMA kernel where the chain has reserved CUs at p = 1
-  // (scripts/r5_split2.sh / r5_latglds.sh, one box, two repetitions): N = 8192 24.58 / 24.55 ->
+  // (scripts/runs/r5_split2.sh / r5_latglds.sh, one box, two repetitions): N = 8192 24.58 / 24.55 ->
   // 24.38 / 24.34 ms, N = 16384 152.2 / 152.0 -> 152.4 / 152.1; without a reservation (N = 32768)
   // 1100.1 / 1100.2 -> 1105.6 / 1101.4 ms, emulated p = 4 / 8 even.  GJ_LAT_GLDS=0/1 overrides.
   lat_wide_ = reserved_cus_ > 0 && L_.p == 1;
