@@ -68,7 +68,7 @@ def parse_args(argv=None):
     ap.add_argument("--bcast", choices=["auto", "ring", "direct"], default=None,
                     help="pivot-row broadcast at p > 2 (default: GJ_BCAST or auto = both timed at "
                          "engine setup, the faster kept)")
-    ap.add_argument("--gemm-variant", default=None, help="big | narrow | tall (kernel tile config)")
+    ap.add_argument("--gemm-variant", default=None, help="big | narrow | squarepf | bigpf | glds | auto (tile for every launch; microbenchmarks)")
     ap.add_argument("--device", choices=["gpu", "cpu"], default="gpu",
                     help="cpu = the native host executor with gloo collectives (rehearses the exact "
                          "multi-rank script on a machine without GPUs; not a performance mode)")
