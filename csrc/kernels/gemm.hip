@@ -565,12 +565,16 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
   const int cvoff = (rlane * ldc + clane) * ES;
 
   acc_t acc[MI][NJ];
+  // the accumulator's input: C itself, or GemmExtra::c_in (ld ldcin)
+  const int ldi = g.cin ? (int)g.ldcin : ldc;
+  const __amdgpu_buffer_rsrc_t rci = g.cin ? rsrc(static_cast<const double*>(g.cin) + m0 * g.ldcin + n0) : rc;
+  const int civoff = (rlane * ldi + clane) * ES;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = rlane + i * 16 + MF::rq(q);
-      const int soff = (i * 16 + MF::rq(q)) * ldc * ES;
+      const int soff = (i * 16 + MF::rq(q)) * ldi * ES;
       bool zrow = false;
 #pragma unroll
       for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) zrow |= (r >= zr0[z] && r < zr1[z]);
@@ -579,7 +583,7 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
         const int c = clane + j * 16;
         if (MODE == MODE_ACC) {
           const bool ok = r < Mt && c < Nt && !zrow && !(c >= z0 && c < z1);
-          acc[i][j][q] = bload<double>(rc, ok ? cvoff + j * 16 * ES : kOOB, soff);
+          acc[i][j][q] = bload<double>(rci, ok ? civoff + j * 16 * ES : kOOB, soff);
         } else {
           acc[i][j][q] = 0.0;
         }
@@ -895,6 +899,9 @@ __global__ __launch_bounds__(glds32::NT, OCC) void gemm_glds_f32(GemmArgs g) {
   const int cvoff = (rlane * ldc + clane) * ES;
 
   acc_t acc[MI][NJ];
+  const int ldi = g.cin ? (int)g.ldcin : ldc;  // the accumulator's input: C or GemmExtra::c_in
+  const __amdgpu_buffer_rsrc_t rci = g.cin ? rsrc(static_cast<const float*>(g.cin) + m0 * g.ldcin + n0) : rc;
+  const int civoff = (rlane * ldi + clane) * ES;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -909,7 +916,7 @@ __global__ __launch_bounds__(glds32::NT, OCC) void gemm_glds_f32(GemmArgs g) {
         const int c = clane + j * 32;
         if (MODE == MODE_ACC) {
           const bool ok = r < Mt && c < Nt && !zrow && !(c >= z0 && c < z1);
-          acc[i][j][q] = bload<float>(rc, ok ? cvoff + j * 32 * ES : kOOB, dr * ldc * ES);
+          acc[i][j][q] = bload<float>(rci, ok ? civoff + j * 32 * ES : kOOB, dr * ldi * ES);
         } else {
           acc[i][j][q] = 0.0f;
         }
@@ -1117,7 +1124,7 @@ void set_lat_glds(int on) { g_lat_glds = on ? 1 : 0; }
 template <typename T, int AL, int MODE>
 static bool try_glds(const GemmArgs& a, hipStream_t s) {
   if constexpr (AL == 1 && MODE != MODE_RESID) {
-    if (a.cin) return false;
+    if (a.cin && a.ldcin * 128 * (int64_t)sizeof(T) >= kRecords) return false;
     if constexpr (sizeof(T) == 8) {
       if (glds_ok(a)) {
         launch_glds<MODE>(a, s);
@@ -1148,7 +1155,11 @@ static void launch(const GemmArgs& a, hipStream_t s) {
     if (lat_glds(a) && a.M >= kLatGldsRows && gemm_variant() == kAutoVariant && try_glds<T, AL, MODE>(a, s)) return;
     return launch_cfg<T, AL, MODE, CfgSmall>(a, s);
   }
-  if (a.cin) return launch_cfg<T, AL, MODE, CfgNarrow>(a, s);  // C_in: register-staged tiles only
+  // C_in (the chunk pass's normalisation input): the LDS-DMA kernels take it too since round 5 --
+  // COMM's 128 x W x j m products ran 90-100 us on the register-staged tile at N = 8192
+  static const bool cin_glds = !getenv("GJ_CIN_GLDS") || std::atoi(getenv("GJ_CIN_GLDS")) != 0;  // A/B knob
+  if (a.cin && cin_glds && gemm_variant() == kAutoVariant && try_glds<T, AL, MODE>(a, s)) return;
+  if (a.cin) return launch_cfg<T, AL, MODE, CfgNarrow>(a, s);
   int v = gemm_variant();
   int fallback = sizeof(T) == 8 ? 9 : 6;  // when the LDS-DMA kernel cannot take the shape
   if (v == kAutoVariant) {

@@ -1,0 +1,27 @@
+#!/bin/bash
+# CHAIN stream A/B: the owners' small chain launches on the reserved CUs (GJ_CHAIN_STREAM=1, auto
+# under a reservation) vs on SIDE (=0).  Then the GPU tests that cover the engine schedule.
+cd "$(dirname "$0")/../.." || exit 1
+export TMPDIR=/tmp
+o=gpurun_out/chain
+mkdir -p $o
+run() {  # size steps warmup cs
+  GJ_CHAIN_STREAM=$4 timeout -k 10 200 python bench.py --size $1 --steps $2 --warmup $3 --no-residual > $o/b.json 2>&1 || { tail -5 $o/b.json; exit 1; }
+  python3 -c "import json; d=json.loads(open('$o/b.json').read().splitlines()[-1]); print('n=$1 chain_stream=$4', d['ms_per_step'])"
+}
+for rep in 1 2; do for cs in 0 1; do run 8192 20 5 $cs || exit 1; done; done
+for rep in 1 2; do for cs in 0 1; do run 16384 5 2 $cs || exit 1; done; done
+for cs in 0 1; do
+  GJ_CHAIN_STREAM=$cs timeout -k 10 300 python bench/bench_emulate.py --ranks 4 8 --size 16384 --depth 0 --bw 50 --bcast direct --reps 1 > $o/emu.txt 2>&1 || { tail -5 $o/emu.txt; exit 1; }
+  echo "emu16k chain_stream=$cs"; grep -h '"p"' $o/emu.txt | python3 -c "
+import sys, json
+for l in sys.stdin:
+    d = json.loads(l); print(d['p'], d.get('bcast', 'free'), d['seconds'])"
+  GJ_CHAIN_STREAM=$cs timeout -k 10 300 python bench/bench_emulate.py --ranks 8 --size 32768 --depth 0 --bw 50 --bcast direct --reps 1 > $o/emu.txt 2>&1 || { tail -5 $o/emu.txt; exit 1; }
+  echo "emu32k chain_stream=$cs"; grep -h '"p"' $o/emu.txt | python3 -c "
+import sys, json
+for l in sys.stdin:
+    d = json.loads(l); print(d['p'], d.get('bcast', 'free'), d['seconds'])"
+done
+GJ_CHAIN_STREAM=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $o/prof8k -o run -- python3 bench.py --size 8192 --steps 5 --warmup 2 --no-residual > $o/prof.log 2>&1 || { tail -5 $o/prof.log; exit 1; }
+python3 scripts/side_chain.py $o/prof8k/run_results.db > $o/side.md; head -16 $o/side.md
