@@ -1,6 +1,8 @@
 // Shader-clock timeline of the matrix-core block inverse (workgroup 0): per pivot step, per panel.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DGJ_BI_PROBE -Icsrc/include -Icsrc/kernels \
-//         bench/blockinv_mfma_probe.hip -o build/blockinv_mfma_probe
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DGJ_BI_PROBE [-DGJ_BI_PROBE_STEPS] -Icsrc/include \
+//         -Icsrc/kernels bench/blockinv_mfma_probe.hip -o build/blockinv_mfma_probe
+// (GJ_BI_PROBE_STEPS adds a stamp per pivot step: a memtime read + store each, so the step times it
+// prints include that perturbation; compare the panel totals of the two builds)
 #include "../csrc/kernels/blockinv_mfma.hip"
 
 #include <cstdio>
@@ -29,7 +31,8 @@ static void run(int m, int nblk) {
     (void)hipEventCreate(&e1);
     (void)hipEventRecord(e0, 0);
     hipLaunchKernelGGL((block_inverse_mfma_kernel<double, MP, LAY>), dim3(nblk), dim3(64 * bim_hw_waves<MP, LAY>()), 0, 0, Lt,
-                       (int64_t)nblk * m, inv, scores, valid, used, m, (int64_t)1, (int64_t)0, 1e-12, nullptr);
+                       (int64_t)nblk * m, inv, scores, valid, used, m, (int64_t)1, (int64_t)0, 1e-12, nullptr,
+                       gj::PivotSelectArgs{}, 0);
     (void)hipEventRecord(e1, 0);
     (void)hipDeviceSynchronize();
     float ms = 0;
@@ -45,6 +48,11 @@ static void run(int m, int nblk) {
       const unsigned long long* P = pr + 8 + 24 * q;
       std::printf("  panel %d: pivot wave start %.0f, factor+publish %.0f, B1 wait %.0f\n", q, P[0] - t0,
                   (double)(P[17] - P[0]), (double)(P[18] - P[17]));
+#ifdef GJ_BI_PROBE_STEPS
+      std::printf("           steps:");
+      for (int j = 0; j < 16; ++j) std::printf(" %.0f", (double)((j < 15 ? P[2 + j] : P[17]) - P[1 + j]));
+      std::printf("\n");
+#endif
       const unsigned long long* B = pr + 520 + 8 * q;
       std::printf("           block w0: apply %.0f, Xn %.0f, wait B1 %.0f, next tile %.0f, wait B0 %.0f\n",
                   (double)(B[1] - B[0]), (double)(B[2] - B[1]), (double)(B[3] - B[2]),

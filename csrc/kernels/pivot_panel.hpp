@@ -23,6 +23,28 @@ namespace kern {
 // sched_barrier: a single in-order wave only hides latency with independent work placed
 // between the dependent instructions).
 #define GJ_SB() __builtin_amdgcn_sched_barrier(0)
+// GJ_PP_PIN: pin every pending-update FMA result and every wave-max stage (empty volatile asm on the
+// register): IR-level code motion otherwise sinks the FMAs below the whole argmax, which then runs
+// with an s_nop in each DPP hazard slot instead of the interleaved update
+#ifndef GJ_PP_PIN
+#define GJ_PP_PIN 1
+#endif
+template <typename X>
+__device__ __forceinline__ void pp_pin(X& x) {
+  if constexpr (GJ_PP_PIN) asm volatile("" : "+v"(x));
+}
+
+#ifdef GJ_BI_PROBE_STEPS  // per-step shader-clock stamps of workgroup 0 (bench/blockinv_mfma_probe.hip)
+extern __device__ unsigned long long g_bim_probe[1024];
+#define GJ_PP_PROBE(slot)                                                                     \
+  do {                                                                                        \
+    if (blockIdx.x == 0 && lane == 0) g_bim_probe[(slot)] = __builtin_amdgcn_s_memtime();     \
+  } while (0)
+#else
+#define GJ_PP_PROBE(slot) \
+  do {                    \
+  } while (0)
+#endif
 
 // Column kk of the pending update of step PJ at list position e: column PJ+2 first, then the
 // others in order (PJ, PJ+1 excluded); -1 past the end.
@@ -66,6 +88,10 @@ struct PivotPanel {
   T up[RPL];  // multipliers of the previous step (its update is still pending)
   T rvp[16];  // the previous step's pivot row (wave-uniform)
   T rv[16];   // this step's pivot row
+  // singular-step flag, OR-ed per step and pinned in a VGPR: left to the compiler, the 16 steps'
+  // comparisons were sunk to the end of the panel, every step's pivot value kept live until then
+  // (SGPR spills to VGPR lanes: ~100 v_readlane / v_writelane per panel)
+  uint32_t singv = 0;
 
   __device__ __forceinline__ PivotPanel(T (&W_)[RPL][16], uint64_t (&km)[RPL], int (&pos_)[RPL], int (&rr_)[16],
                                         bool& sg, int lane_, int c0_, int m_, double th)
@@ -75,7 +101,10 @@ struct PivotPanel {
   __device__ __forceinline__ void upd() {
     if constexpr (COL >= 0) {
 #pragma unroll
-      for (int s = 0; s < RPL; ++s) W[s][COL] = __builtin_fma(up[s], rvp[COL], W[s][COL]);
+      for (int s = 0; s < RPL; ++s) {
+        W[s][COL] = __builtin_fma(up[s], rvp[COL], W[s][COL]);
+        pp_pin(W[s][COL]);
+      }
     }
   }
   // chunk C (0..6) of the pending update of step PJ: two columns; chunk 6 also stores column PJ
@@ -143,6 +172,7 @@ struct PivotPanel {
   template <int J>
   __device__ __forceinline__ void step() {
     constexpr int PJ = J - 1;
+    GJ_PP_PROBE(9 + 24 * (c0 / 16) + J);
     // argmax of column J (exact: see wave_pivot_row_u64), step J-1's update in its gaps
     uint64_t key[RPL];
     uint32_t v = 0;
@@ -153,20 +183,25 @@ struct PivotPanel {
     }
     work<PJ, 0>();
     v = umax32(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true));
+    pp_pin(v);
     GJ_SB();
     work<PJ, 1>();
     v = umax32(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true));
+    pp_pin(v);
     GJ_SB();
     work<PJ, 2>();
     v = umax32(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true));
+    pp_pin(v);
     GJ_SB();
     work<PJ, 3>();
     v = umax32(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true));
+    pp_pin(v);
     GJ_SB();
     work<PJ, 4>();
     {
       const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
       v = umax32(p[0], p[1]);
+      pp_pin(v);
     }
     GJ_SB();
     work<PJ, 5>();
@@ -232,7 +267,8 @@ struct PivotPanel {
     // pivot value, next column's entry, reciprocal; the pivot-row reads in its gaps
     T piv, nx, inv;
     chain_sel<0, J>(rs, rl, piv, nx, inv);  // rs is wave-uniform
-    sing |= (c0 + J < m) && (none || !(fabs((double)piv) >= thresh));
+    singv |= ((c0 + J < m) && (none || !(fabs((double)piv) >= thresh))) ? 1u : 0u;
+    asm volatile("" : "+v"(singv));
     T u[RPL];
 #pragma unroll
     for (int s = 0; s < RPL; ++s) u[s] = (lane + 64 * s == r) ? inv - T(1) : -W[s][J] * inv;
@@ -250,6 +286,7 @@ struct PivotPanel {
   template <int... J>
   __device__ __forceinline__ void run(std::integer_sequence<int, J...>) {
     (step<J>(), ...);
+    sing = sing || (singv != 0);
     // the last step's update (no next argmax to hide it in)
 #pragma unroll
     for (int c = 0; c < 15; ++c) {
