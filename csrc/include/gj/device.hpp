@@ -55,6 +55,10 @@ struct GemmExtra {
   void* tneg = nullptr;
   int64_t ldtneg = 0;
   int64_t tneg_cols = 0;
+  // Output columns [skip_c0, skip_c1) are neither read nor written (nor are those columns of B):
+  // one launch for a chunk whose middle columns another stream updates (the trailing update around
+  // the look-ahead columns).  GPU: whole tiles, so both bounds multiples of Device::skip_align().
+  int64_t skip_c0 = 0, skip_c1 = 0;
   // Owner-predicated launch (the host-free pivot chain at p > 1): the GEMM does nothing unless this
   // rank owns the pivot g = *owner_phys (g % owner_p == owner_k) -- read on the device.
   const int32_t* owner_phys = nullptr;
@@ -177,6 +181,8 @@ class Device {
   // always find idle CUs (the first n bits of the CU mask; n = 32 is one CU per shader engine).
   // Returns the number of CUs actually reserved.  Call while the device is idle.
   virtual int reserve_cus(int n) { (void)n; return 0; }
+  // alignment (columns) of GemmExtra::skip_c0 / skip_c1 this device honours
+  virtual int64_t skip_align() const { return 1; }
 
   // ---- schedule-checking hooks (RaceCheckDevice, gj/race_check.hpp; no-ops elsewhere) ----
   // Where the caller is (read at every op for reports): its step counter and phase name.

@@ -300,6 +300,9 @@ class Engine {
   // the pivot chain's column updates (rows x m x j m) on the LDS-DMA kernel instead of the 64 x 32
   // latency tile (GemmExtra::lat_wide): on when CUs are reserved for the chain at p = 1
   bool lat_wide_ = false;
+  // MAIN's chunk update as one launch around the look-ahead columns (GemmExtra::skip_c0/c1) instead
+  // of one launch per side (GJ_SKIP_COLS=0)
+  bool skip_cols_ = true;
   std::vector<char> used_local_;       // local blocks used as pivot rows so far (host copy)
   GemmExtra chain_sel_[2], defer_sel_[2];  // by panel parity; rsel_m == 0: panel without a split
   void deferred_updates(int64_t v, int stream);

@@ -174,6 +174,7 @@ class RaceCheckDevice : public Device {
   void wait_mark(int s, const std::shared_ptr<void>& h) override;
   void occupy(int s, int nwg, double us, int lds_bytes = 0) override;
   int reserve_cus(int n) override { return inner_->reserve_cus(n); }
+  int64_t skip_align() const override { return inner_->skip_align(); }
 
   void trace_context(const int64_t* step, const char* const* phase) override {
     step_ = step;

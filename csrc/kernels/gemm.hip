@@ -151,6 +151,7 @@ struct GemmArgs {
   bool dense;           // GemmExtra::dense: the 5-workgroups-per-CU LDS-DMA build
   uint64_t rsel[GemmExtra::kRselWords];  // GemmExtra::rsel / rsel_m: row-block selection
   int64_t rsel_m;
+  int64_t skc0, skc1;   // GemmExtra::skip_c0 / skip_c1 (whole tiles)
   const void* cin;      // GemmExtra::c_in (MODE_ACC input array, ld ldcin; null: C itself)
   int64_t ldcin;
 };
@@ -200,6 +201,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& g, const int tile) {
   __shared__ T ldsB[2][BK][CF::LDB];  // B slices
 
   const int tm = tile / g.tiles_n, tn = tile % g.tiles_n;
+  if ((int64_t)tn * BN >= g.skc0 && (int64_t)(tn + 1) * BN <= g.skc1) return;  // GemmExtra::skip_c0/c1
   // m0L: the tile's first row among the M rows of the product; m0: its physical row (they differ
   // only under a row-block selection, GemmExtra::rsel)
   const int64_t m0L = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
@@ -537,6 +539,7 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
   const int gsz = (g.tiles_m - gr0) < G ? (g.tiles_m - gr0) : G;
   const int rem = tile - grp * G * g.tiles_n;
   const int tm = gr0 + rem % gsz, tn = rem / gsz;
+  if ((int64_t)tn * BN >= g.skc0 && (int64_t)(tn + 1) * BN <= g.skc1) return;  // GemmExtra::skip_c0/c1
   // m0L logical / m0 physical first row (GemmExtra::rsel, as in gemm_tile)
   const int64_t m0L = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
   const int64_t m0 = g.rsel_m > 0 ? rsel_map(g, m0L) : m0L;
@@ -871,6 +874,7 @@ __global__ __launch_bounds__(glds32::NT, OCC) void gemm_glds_f32(GemmArgs g) {
   const int gsz = (g.tiles_m - gr0) < G ? (g.tiles_m - gr0) : G;
   const int rem = tile - grp * G * g.tiles_n;
   const int tm = gr0 + rem % gsz, tn = rem / gsz;
+  if ((int64_t)tn * BN >= g.skc0 && (int64_t)(tn + 1) * BN <= g.skc1) return;  // GemmExtra::skip_c0/c1
   // m0L logical / m0 physical first row (GemmExtra::rsel, as in gemm_tile)
   const int64_t m0L = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
   const int64_t m0 = g.rsel_m > 0 ? rsel_map(g, m0L) : m0L;
@@ -1212,6 +1216,10 @@ static void fill_extra(GemmArgs& a, const GemmExtra* ex) {
   a.dense = ex ? ex->dense : false;
   a.rsel_m = ex ? ex->rsel_m : 0;
   a.cin = ex ? ex->c_in : nullptr;
+  a.skc0 = ex ? ex->skip_c0 : 0;
+  a.skc1 = ex ? ex->skip_c1 : 0;
+  if (a.skc1 > a.skc0 && (a.skc0 % 128 != 0 || a.skc1 % 128 != 0))
+    throw Error(Status::BadArgs, "gemm: skip columns must be multiples of 128");
   a.ldcin = ex ? ex->ldc_in : 0;
   for (int w = 0; w < GemmExtra::kRselWords; ++w) a.rsel[w] = ex ? ex->rsel[w] : 0;
 }

@@ -194,9 +194,11 @@ PYBIND11_MODULE(_C, mod) {
               int64_t N, int64_t K, U A, int64_t lda, U B, int64_t ldb, U C, int64_t ldc, int64_t zc0,
               int64_t zc1, std::vector<int64_t> zero_rows, int64_t zh, U tneg, int64_t ldtneg, bool latency,
               int64_t tneg_cols, bool dense, U c_in, int64_t ldc_in, std::vector<int64_t> row_blocks,
-              int64_t row_block_m) {
+              int64_t row_block_m, int64_t skip_c0, int64_t skip_c1) {
              GemmExtra ex;
              ex.dense = dense;
+             ex.skip_c0 = skip_c0;
+             ex.skip_c1 = skip_c1;
              ex.c_in = (const void*)c_in;
              ex.ldc_in = ldc_in;
              if (row_block_m > 0) {  // GemmExtra::rsel from a list of selected row blocks
@@ -227,7 +229,8 @@ PYBIND11_MODULE(_C, mod) {
            py::arg("zc0") = 0, py::arg("zc1") = 0, py::arg("zero_rows") = std::vector<int64_t>(),
            py::arg("zh") = 0, py::arg("tneg") = U(0), py::arg("ldtneg") = 0, py::arg("latency") = false,
            py::arg("tneg_cols") = 0, py::arg("dense") = false, py::arg("c_in") = U(0), py::arg("ldc_in") = 0,
-           py::arg("row_blocks") = std::vector<int64_t>(), py::arg("row_block_m") = 0)
+           py::arg("row_blocks") = std::vector<int64_t>(), py::arg("row_block_m") = 0, py::arg("skip_c0") = 0,
+           py::arg("skip_c1") = 0)
       .def("gemm_batch",
            [](Device& d, const std::string& dt,
               const std::vector<std::tuple<std::string, int64_t, int64_t, int64_t, U, int64_t, U, int64_t,

@@ -62,18 +62,23 @@ void gemm_t(GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const T* A, 
       const double a = (al == ALayout::RowMajor) ? (double)A[i * lda + k] : (double)A[k * lda + i];
       if (a == 0.0) continue;
       const T* b = B + k * ldb;
-      for (int64_t j = 0; j < N; ++j) acc[j] += a * (double)b[j];
+      for (int64_t j = 0; j < N; ++j)
+        if (!(j >= ex.skip_c0 && j < ex.skip_c1)) acc[j] += a * (double)b[j];
     }
     T* c = C + i * ldc;
     const T* ci = ex.c_in ? static_cast<const T*>(ex.c_in) + i * ex.ldc_in : c;  // GemmExtra::c_in
-    if (op == GemmOp::Acc)
+    const auto skip = [&](int64_t j) { return j >= ex.skip_c0 && j < ex.skip_c1; };  // GemmExtra::skip_c0/c1
+    if (op == GemmOp::Acc) {
       for (int64_t j = 0; j < N; ++j)
-        c[j] = (T)((zrow || (j >= ex.zc0 && j < ex.zc1) ? 0.0 : (double)ci[j]) + acc[j]);
-    else
-      for (int64_t j = 0; j < N; ++j) c[j] = (T)acc[j];
+        if (!skip(j)) c[j] = (T)((zrow || (j >= ex.zc0 && j < ex.zc1) ? 0.0 : (double)ci[j]) + acc[j]);
+    } else {
+      for (int64_t j = 0; j < N; ++j)
+        if (!skip(j)) c[j] = (T)acc[j];
+    }
     if (ex.tneg) {
       const int64_t nt = ex.tneg_cols > 0 ? std::min(ex.tneg_cols, N) : N;
-      for (int64_t j = 0; j < nt; ++j) static_cast<T*>(ex.tneg)[j * ex.ldtneg + i] = -c[j];
+      for (int64_t j = 0; j < nt; ++j)
+        if (!skip(j)) static_cast<T*>(ex.tneg)[j * ex.ldtneg + i] = -c[j];
     }
   });
 }

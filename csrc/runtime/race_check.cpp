@@ -372,13 +372,24 @@ void gemm_acc(std::vector<Acc>& a, DType dt, GemmOp op, ALayout al, int64_t M, i
     if (ex.owner_phys) a.push_back(R(span(ex.owner_phys, 4), "owner"));
     return;
   }
-  if (K > 0) {
-    a.push_back(R(al == ALayout::KMajor ? rect(A, lda, M, K, es) : rect(A, lda, K, M, es), "A"));
-    a.push_back(R(rect(B, ldb, N, K, es), "B"));
+  // column ranges touched: [0, N) minus GemmExtra::skip_c0 / skip_c1
+  int64_t cr0[2] = {0, 0}, cr1[2] = {N, 0};
+  int ncr = 1;
+  if (ex.skip_c1 > ex.skip_c0) {
+    cr1[0] = std::min(N, ex.skip_c0);
+    cr0[1] = ex.skip_c1;
+    cr1[1] = N;
+    ncr = 2;
   }
+  if (K > 0) a.push_back(R(al == ALayout::KMajor ? rect(A, lda, M, K, es) : rect(A, lda, K, M, es), "A"));
   (void)op;  // C += AB reads C too; a write of the same bytes already conflicts with any access
-  a.push_back(W(rect(C, ldc, N, M, es), "C"));
-  if (ex.c_in) a.push_back(R(rect(ex.c_in, ex.ldc_in, N, M, es), "C_in"));
+  for (int z = 0; z < ncr; ++z) {
+    const int64_t w = cr1[z] - cr0[z];
+    if (w <= 0) continue;
+    if (K > 0) a.push_back(R(rect(static_cast<const char*>(B) + cr0[z] * es, ldb, w, K, es), "B"));
+    a.push_back(W(rect(static_cast<char*>(C) + cr0[z] * es, ldc, w, M, es), "C"));
+    if (ex.c_in) a.push_back(R(rect(static_cast<const char*>(ex.c_in) + cr0[z] * es, ex.ldc_in, w, M, es), "C_in"));
+  }
   if (ex.tneg) {
     const int64_t cols = ex.tneg_cols > 0 ? std::min(ex.tneg_cols, N) : N;
     a.push_back(W(rect(ex.tneg, ex.ldtneg, M, cols, es), "tneg"));

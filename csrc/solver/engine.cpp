@@ -233,6 +233,7 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // (scripts/runs/r5_split2.sh / r5_latglds.sh, one box, two repetitions): N = 8192 24.58 / 24.55 ->
   // 24.38 / 24.34 ms, N = 16384 152.2 / 152.0 -> 152.4 / 152.1; without a reservation (N = 32768)
   // 1100.1 / 1100.2 -> 1105.6 / 1101.4 ms, emulated p = 4 / 8 even.  GJ_LAT_GLDS=0/1 overrides.
+  if (const char* e = std::getenv("GJ_SKIP_COLS")) skip_cols_ = std::atoi(e) != 0;
   lat_wide_ = reserved_cus_ > 0 && L_.p == 1;
   if (const char* e = std::getenv("GJ_LAT_GLDS")) lat_wide_ = std::atoi(e) != 0;
   split_ = 0;
@@ -1200,15 +1201,29 @@ void Engine::big_update(int64_t u) {
               W * (int64_t)esz(), m, ms);
     const int pe = prof_begin(ms);
     int64_t ra[2], rb[2], nr = 0;
+    // the look-ahead columns [x0, x1) are done: one launch around them (GemmExtra::skip_c0/c1) when
+    // the device can skip whole tiles there, else one launch per side.  N = 8192: the two launches
+    // of a split chunk took 346-353 us against 321 us for one launch of the same tiles (two launch
+    // tails), profiles/side_chain_r5.md
+    int64_t sk0 = 0, sk1 = 0;
     if (has_next && x0 >= c0 && x0 < c1) {
-      if (x0 > c0) { ra[nr] = c0; rb[nr] = x0; ++nr; }
-      if (c1 > x1) { ra[nr] = x1; rb[nr] = c1; ++nr; }
+      const int64_t al = dev_.skip_align();
+      if ((x0 - c0) % al == 0 && (x1 - c0) % al == 0 && x1 <= c1 && skip_cols_) {
+        ra[0] = c0; rb[0] = c1; nr = 1;
+        sk0 = x0 - c0;
+        sk1 = x1 - c0;
+      } else {
+        if (x0 > c0) { ra[nr] = c0; rb[nr] = x0; ++nr; }
+        if (c1 > x1) { ra[nr] = x1; rb[nr] = c1; ++nr; }
+      }
     } else {
       ra[0] = c0; rb[0] = c1; nr = 1;
     }
     if (rows > 0)
       for (int64_t z = 0; z < nr; ++z) {
         GemmExtra ex = prows;
+        ex.skip_c0 = sk0;
+        ex.skip_c1 = sk1;
         ex.zc0 = pc0 - ra[z];  // the panel's own block columns enter as 0
         ex.zc1 = pc1 - ra[z];
         // with CUs reserved for the pivot chain the trailing update may fill the rest densely:

@@ -39,7 +39,7 @@ def _p(t: torch.Tensor) -> int:
 def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, op: str = "acc", a_kmajor: bool = False,
          zero_cols=(0, 0), zero_rows=(), zero_row_height: int = 0, tneg: torch.Tensor = None,
          latency: bool = False, dense: bool = False, c_in: torch.Tensor = None, row_blocks=None,
-         row_block_m: int = 0) -> torch.Tensor:
+         row_block_m: int = 0, skip_cols=(0, 0)) -> torch.Tensor:
     """C += A@B (op="acc") or C = A@B (op="store").  With a_kmajor, ``A`` is given as A^T (K x M).
 
     Elimination extras (op="acc"): C enters as 0 in the columns ``zero_cols`` = (c0, c1) and in the
@@ -50,7 +50,9 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, op: str = "acc", a_k
     trailing update (the engine's choice under a CU reservation).  ``c_in`` (op="acc"): the
     accumulator's input array instead of C itself (C = c_in + A@B).  ``row_blocks`` with
     ``row_block_m``: only those row blocks of C / A^T take part (GemmExtra::rsel); M = C's rows is
-    then the physical height and the product runs over len(row_blocks) * row_block_m rows."""
+    then the physical height and the product runs over len(row_blocks) * row_block_m rows.
+    ``skip_cols`` = (s0, s1): those output columns are neither read nor written (GemmExtra::skip_c0
+    / skip_c1; multiples of 128 on the GPU)."""
     assert A.dtype == B.dtype == C.dtype and A.stride(-1) == 1 and B.stride(-1) == 1 and C.stride(-1) == 1
     M, N = C.shape
     K = A.shape[0] if a_kmajor else A.shape[1]
@@ -67,7 +69,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor, op: str = "acc", a_k
     device_for(C).gemm(_DT[C.dtype], op, a_kmajor, Msel, N, K, _p(A), A.stride(0), _p(B), B.stride(0), _p(C),
                        C.stride(0), int(zero_cols[0]), int(zero_cols[1]), [int(r) for r in zero_rows],
                        int(zero_row_height), tp, ldt, bool(latency), tcols, bool(dense), cp, ldci, rb,
-                       int(row_block_m))
+                       int(row_block_m), int(skip_cols[0]), int(skip_cols[1]))
     return C
 
 

@@ -1,0 +1,27 @@
+#!/bin/bash
+# One MAIN launch per chunk around the look-ahead columns (GemmExtra::skip_c0/c1) vs one per side.
+cd "$(dirname "$0")/../.." || exit 1
+export TMPDIR=/tmp
+o=gpurun_out/skip
+mkdir -p $o
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "skip or row_blocks" > $o/tests.txt 2>&1 || { tail -30 $o/tests.txt; exit 1; }
+tail -1 $o/tests.txt
+run() {  # size steps warmup skip
+  GJ_SKIP_COLS=$4 timeout -k 10 200 python bench.py --size $1 --steps $2 --warmup $3 --no-residual > $o/b.json 2>&1 || { tail -5 $o/b.json; exit 1; }
+  python3 -c "import json; d=json.loads(open('$o/b.json').read().splitlines()[-1]); print('n=$1 skip=$4', d['ms_per_step'])"
+}
+for rep in 1 2; do for k in 0 1; do run 8192 20 5 $k || exit 1; done; done
+for rep in 1 2; do for k in 0 1; do run 16384 5 2 $k || exit 1; done; done
+for rep in 1 2; do for k in 0 1; do run 32768 3 1 $k || exit 1; done; done
+for k in 0 1; do
+  GJ_SKIP_COLS=$k timeout -k 10 300 python bench/bench_emulate.py --ranks 4 8 --size 16384 --depth 0 --bw 50 --bcast direct --reps 1 > $o/emu.txt 2>&1 || { tail -5 $o/emu.txt; exit 1; }
+  echo "emu16k skip=$k"; grep -h '"p"' $o/emu.txt | python3 -c "
+import sys, json
+for l in sys.stdin:
+    d = json.loads(l); print(d['p'], d.get('bcast', 'free'), d['seconds'])"
+  GJ_SKIP_COLS=$k timeout -k 10 300 python bench/bench_emulate.py --ranks 8 --size 32768 --depth 0 --bw 50 --bcast direct --reps 1 > $o/emu.txt 2>&1 || { tail -5 $o/emu.txt; exit 1; }
+  echo "emu32k skip=$k"; grep -h '"p"' $o/emu.txt | python3 -c "
+import sys, json
+for l in sys.stdin:
+    d = json.loads(l); print(d['p'], d.get('bcast', 'free'), d['seconds'])"
+done

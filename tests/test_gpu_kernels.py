@@ -558,3 +558,34 @@ def test_gemm_glds_dense_build(native, M, N, K, dense):
     ops.gemm(A.t().contiguous().cuda(), B.cuda(), Cd, op="acc", a_kmajor=True, zero_cols=(z0, z1), zero_rows=zr,
              zero_row_height=zh, dense=dense)
     assert (Cd.cpu() - ref).abs().max().item() < 1e-12 * K
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("variant", ["auto", "narrow"])
+@pytest.mark.parametrize("latency", [False, True])
+def test_gemm_skip_columns(dtype, variant, latency, native):
+    """GemmExtra::skip_c0 / skip_c1 (MAIN's chunk update around the look-ahead columns): the skipped
+    output columns keep their bytes, every other column equals the full product bit for bit."""
+    M, N, K = 512, 640, 256
+    A = _rand((K, M), torch.float64, 61).to(dtype).cuda()
+    B = _rand((K, N), torch.float64, 62).to(dtype).cuda()
+    C = _rand((M, N), torch.float64, 63).to(dtype).cuda()
+    T = torch.full((128, M), 7.0, dtype=dtype, device="cuda") if dtype == torch.float64 else None
+    native.set_gemm_variant(variant)
+    try:
+        full = C.clone()
+        Tf = T.clone() if T is not None else None
+        ops.gemm(A, B, full, op="acc", a_kmajor=True, latency=latency, tneg=Tf, zero_cols=(64, 192))
+        got = C.clone()
+        ops.gemm(A, B, got, op="acc", a_kmajor=True, latency=latency, tneg=T, zero_cols=(64, 192),
+                 skip_cols=(128, 384))
+    finally:
+        native.set_gemm_variant("auto")
+    keep = torch.zeros(N, dtype=torch.bool, device="cuda")
+    keep[128:384] = True
+    assert torch.equal(got[:, keep], C[:, keep])
+    assert torch.equal(got[:, ~keep], full[:, ~keep])
+    if T is not None:  # -C^T of the first 128 columns: outside the skipped range, written
+        assert torch.equal(T, Tf)
+    with pytest.raises(Exception, match="multiples of 128"):
+        ops.gemm(A, B, C.clone(), op="acc", a_kmajor=True, skip_cols=(64, 128))
