@@ -202,6 +202,8 @@ class Engine {
     std::string fault_injection;  // active GJ_TEST_* knobs ("" in every normal run)
     int split = 0;                // chain / deferred split of the column updates (split_: 0, 1, 2)
     bool lat_wide = false;        // chain column updates on the LDS-DMA kernel (lat_wide_)
+    bool skip_cols = false;       // one MAIN launch per chunk around the look-ahead columns (skip_cols_)
+    bool chunk_skip = false;      // one chunk-pass launch per step around the panel columns (chunk_skip_)
   };
   Policy policy() const;
   const std::string& bcast_algo() const { return bcast_algo_; }  // "ring" | "direct"
@@ -301,8 +303,11 @@ class Engine {
   // latency tile (GemmExtra::lat_wide): on when CUs are reserved for the chain at p = 1
   bool lat_wide_ = false;
   // MAIN's chunk update as one launch around the look-ahead columns (GemmExtra::skip_c0/c1) instead
-  // of one launch per side (GJ_SKIP_COLS=0)
-  bool skip_cols_ = true;
+  // of one launch per side: on under a CU reservation (GJ_SKIP_COLS=0/1 overrides)
+  bool skip_cols_ = false;
+  // the same for the chunk pass's normalisation GEMMs around the panel / next-panel columns
+  // (follows skip_cols_; GJ_CHUNK_SKIP=0/1 overrides)
+  bool chunk_skip_ = false;
   std::vector<char> used_local_;       // local blocks used as pivot rows so far (host copy)
   GemmExtra chain_sel_[2], defer_sel_[2];  // by panel parity; rsel_m == 0: panel without a split
   void deferred_updates(int64_t v, int stream);

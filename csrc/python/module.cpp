@@ -473,6 +473,8 @@ PYBIND11_MODULE(_C, mod) {
                                if (!pl.fault_injection.empty()) d["fault_injection"] = pl.fault_injection;
                                d["split"] = pl.split;
                                d["lat_wide"] = pl.lat_wide;
+                               d["skip_cols"] = pl.skip_cols;
+                               d["chunk_skip"] = pl.chunk_skip;
                                d["bcast"] = e.eng->bcast_algo();
                                d["bcast_tuning"] = e.comm->bcast_report();
                                d["comm"] = e.comm->describe();

@@ -233,7 +233,14 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // (scripts/runs/r5_split2.sh / r5_latglds.sh, one box, two repetitions): N = 8192 24.58 / 24.55 ->
   // 24.38 / 24.34 ms, N = 16384 152.2 / 152.0 -> 152.4 / 152.1; without a reservation (N = 32768)
   // 1100.1 / 1100.2 -> 1105.6 / 1101.4 ms, emulated p = 4 / 8 even.  GJ_LAT_GLDS=0/1 overrides.
+  // One launch around the look-ahead columns (MAIN) and around the panel / next-panel columns (the
+  // chunk pass) where CUs are reserved for the chain (scripts/runs/r5_skip.sh, r5_skip2.sh): N = 8192
+  // 24.20 -> 23.61 ms, N = 16384 151.5 -> 150.3 ms, emulated p = 8 at N = 16384 -3 %; without a
+  // reservation (N = 32768) the MAIN merge measured +0.1-0.3 % and the chunk-pass merge +1.5 %.
+  skip_cols_ = reserved_cus_ > 0;
   if (const char* e = std::getenv("GJ_SKIP_COLS")) skip_cols_ = std::atoi(e) != 0;
+  chunk_skip_ = skip_cols_;
+  if (const char* e = std::getenv("GJ_CHUNK_SKIP")) chunk_skip_ = std::atoi(e) != 0;
   lat_wide_ = reserved_cus_ > 0 && L_.p == 1;
   if (const char* e = std::getenv("GJ_LAT_GLDS")) lat_wide_ = std::atoi(e) != 0;
   split_ = 0;
@@ -265,6 +272,8 @@ Engine::Policy Engine::policy() const {
   p.fault_injection = fault_injection_;
   p.split = split_;
   p.lat_wide = lat_wide_;
+  p.skip_cols = skip_cols_;
+  p.chunk_skip = chunk_skip_;
   return p;
 }
 
@@ -996,19 +1005,38 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
     // panel's (the look-ahead rows carried them, MAIN's chunk pass skips them, and the look-ahead
     // update on SIDE rewrites X there while this pass runs: reading them would race it)
     int64_t ra[3], rb[3], nr = 0;
+    int64_t sk0 = 0, sk1 = 0;  // or one launch over the chunk that skips the cut (GemmExtra::skip_c0/c1)
     const bool has_panel = (pc0 >= c0 && pc0 < c1);
     {
       int64_t cut0[2], cut1[2], ncut = 0;
       if (has_panel) { cut0[ncut] = pc0; cut1[ncut++] = pc1; }
       if (has_next && !dropped("x")) { cut0[ncut] = xn0; cut1[ncut++] = xn1; }
+      int64_t lo_all = -1, hi_all = -1, nin = 0;
+      bool contiguous = true;
       int64_t a = c0;
       for (int64_t z = 0; z < ncut; ++z) {  // the cuts are ordered (the next panel follows this one)
         const int64_t lo = std::max(cut0[z], c0), hi = std::min(cut1[z], c1);
         if (lo >= hi) continue;
+        if (nin > 0 && lo != hi_all) contiguous = false;
+        if (nin == 0) lo_all = lo;
+        hi_all = hi;
+        ++nin;
         if (lo > a) { ra[nr] = a; rb[nr] = lo; ++nr; }
         a = std::max(a, hi);
       }
       if (c1 > a) { ra[nr] = a; rb[nr] = c1; ++nr; }
+      const int64_t al = dev_.skip_align();
+      // (under a CU reservation only: N = 8192 24.20 -> 23.61 ms with both launches merged, but
+      // N = 32768, where the chunk pass shares the CUs with the trailing update, 1069 -> 1086 ms;
+      // scripts/runs/r5_skip.sh, profiles/side_chain_r5.md)
+      if (nr > 1 && nin > 0 && contiguous && chunk_skip_ && (lo_all - c0) % al == 0 &&
+          (hi_all - c0) % al == 0) {
+        nr = 1;
+        ra[0] = c0;
+        rb[0] = c1;
+        sk0 = lo_all - c0;
+        sk1 = hi_all - c0;
+      }
     }
     char* chunk = rb_chunk(par, c);
     std::vector<BcastOp> bops;
@@ -1034,6 +1062,8 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
         const int64_t sl = r.phys / L_.p;
         GemmExtra lat;
         lat.latency = comm_small_tiles_;
+        lat.skip_c0 = sk0;
+        lat.skip_c1 = sk1;
         for (int64_t z = 0; z < nr; ++z) {
           const int64_t a = ra[z], w = rb[z] - ra[z];
           if (j == 0) {

@@ -171,3 +171,16 @@ def test_split_column_updates_race_free(mode, p, depth, la_side, monkeypatch):
     rep = _run(64 * 11, 64, p, depth=depth, chunk_cols=64 * 3, jitter_us=20.0)
     assert rep["race_count"] == 0, "\n".join(rep["races"])
     assert rep["residual"] < 1e-8
+
+
+@pytest.mark.parametrize("p,depth", [(1, 2), (1, 4), (3, 2), (8, 2), (4, 3)])
+@pytest.mark.parametrize("skip", ["0", "1"])
+def test_skip_columns_race_free(p, depth, skip, monkeypatch):
+    """GJ_SKIP_COLS / GJ_CHUNK_SKIP: MAIN's chunk update and the chunk pass's normalisation as one
+    launch around the look-ahead / panel columns (GemmExtra::skip_c0/c1) or one launch per side:
+    race-free either way, and the same inverse."""
+    monkeypatch.setenv("GJ_SKIP_COLS", skip)
+    monkeypatch.setenv("GJ_CHUNK_SKIP", skip)
+    rep = _run(64 * 11, 64, p, depth=depth, chunk_cols=64 * 4, jitter_us=20.0)
+    assert rep["race_count"] == 0, "\n".join(rep["races"])
+    assert rep["residual"] < 1e-8

@@ -128,3 +128,19 @@ def test_split_policy_reported_and_off_when_not_applicable(native, monkeypatch):
     assert native.Engine(native.host_device(2), native.self_comm(), 600, 64, "fp64").policy["lat_wide"] is False
     monkeypatch.setenv("GJ_LAT_GLDS", "1")
     assert native.Engine(native.host_device(2), native.self_comm(), 600, 64, "fp64").policy["lat_wide"] is True
+
+
+@pytest.mark.parametrize("p,depth", [(1, 2), (3, 3), (8, 2)])
+def test_skip_columns_bit_identical(p, depth, monkeypatch):
+    """One launch around the skipped columns computes the same products as one launch per side."""
+    n, m = 64 * 11, 64
+    out = []
+    for sk in ("0", "1"):
+        monkeypatch.setenv("GJ_SKIP_COLS", sk)
+        monkeypatch.setenv("GJ_CHUNK_SKIP", sk)
+        eng = gj.GaussJordan(block_size=m, ranks=p, device="cpu", comm="async", depth=depth, jitter_us=200.0,
+                             host_threads=2, chunk_cols=64 * 4, extra=dict(verify=True))
+        rep = eng.run(n, gen="random", seed=8, keep_inverse=True)
+        assert rep["status"] == 0, rep["message"]
+        out.append(rep["inverse"])
+    assert np.array_equal(out[0], out[1])
