@@ -202,6 +202,12 @@ class Device {
   // ---- kernels ----
   // X (layout.rows x npad, ld npad) := A' restricted to this rank's block rows.
   virtual void generate(DType dt, void* X, const Layout& L, GenSpec g, int s) = 0;
+  // generate() and out[0] = row_abs_max() of the result (a device may fuse the two passes; the
+  // HIP device does, one read of the matrix less)
+  virtual void generate_norm(DType dt, void* X, const Layout& L, GenSpec g, double* out, int s) {
+    generate(dt, X, L, g, s);
+    row_abs_max(dt, X, L.npad, L, out, s);
+  }
   // X[r][c] := src[r][c] (doubles, ld src_ld) for r < rows, c < cols (dtype conversion).
   virtual void upload_convert(DType dt, void* X, int64_t ldx, const double* src_dev, int64_t src_ld,
                               int64_t rows, int64_t cols, int s) = 0;

@@ -312,6 +312,8 @@ class Engine {
   GemmExtra chain_sel_[2], defer_sel_[2];  // by panel parity; rsel_m == 0: panel without a split
   void deferred_updates(int64_t v, int stream);
   double norm_a_ = -1;
+  double local_norm_ = 0;           // this rank's ||X||_inf part, computed by generate()
+  bool local_norm_valid_ = false;   // X unchanged since generate()
 
   // chunk plan (block-column ranges, multiples of d_ blocks so a panel never straddles chunks)
   std::vector<int64_t> cb0_, cb1_;

@@ -38,6 +38,7 @@ class HipDevice : public Device {
  public:
   int reserve_cus(int n) override;
   int64_t skip_align() const override { return 128; }  // whole tiles of every GEMM kernel
+  void generate_norm(DType dt, void* X, const Layout& L, GenSpec g, double* out, int s) override;
   void sync_stream(int s) override;
   bool stream_idle(int s) override;
   void sync_all() override;

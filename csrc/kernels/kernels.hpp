@@ -73,6 +73,8 @@ size_t block_inverse_iscratch_bytes(const Layout& L);
 
 // misc.hip
 void generate(DType dt, void* X, const Layout& L, int kind, uint64_t seed, hipStream_t s);
+// generate() fused with row_abs_max() of the result (out zeroed here): one pass over the matrix
+void generate_norm(DType dt, void* X, const Layout& L, int kind, uint64_t seed, double* out, hipStream_t s);
 void widen(DType dt, double* dst, int64_t ldd, const void* X, int64_t ldx, int64_t rows, int64_t cols,
            hipStream_t s);
 void upload_convert(DType dt, void* X, int64_t ldx, const double* src, int64_t src_ld, int64_t rows,

@@ -48,6 +48,42 @@ __global__ void generate_kernel(T* X, int64_t rows, int64_t npad, int64_t n, int
   }
 }
 
+// One workgroup per local row: the row's values are generated column by column (no 64-bit index
+// division per element, as in the flat kernel above) and their magnitudes summed in the order of
+// row_abs_kernel below (thread t: columns t, t + 256, ...; then the same wave / workgroup
+// reduction), so the norm is bit-identical to generate() followed by row_abs_max().
+template <typename T>
+__global__ __launch_bounds__(256) void generate_norm_kernel(T* X, int64_t npad, int64_t n, int64_t m, int64_t p,
+                                                            int64_t k, int kind, uint64_t seed, double* out) {
+  const int64_t r = blockIdx.x;
+  const int64_t gr = ((r / m) * p + k) * m + r % m;
+  T* row = X + r * npad;
+  double s = 0.0;
+  for (int64_t j = threadIdx.x; j < npad; j += 256) {
+    const T v = (T)gen_value(kind, seed, n, gr, j);
+    row[j] = v;
+    if (j < n) s += fabs((double)v);
+  }
+  if (gr >= n) return;  // padding row: generated, not part of the norm (row_abs_kernel)
+  __shared__ double sh[4];
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomic_max_nonneg(out, sh[0] + sh[1] + sh[2] + sh[3]);
+}
+
+void generate_norm(DType dt, void* X, const Layout& L, int kind, uint64_t seed, double* out, hipStream_t s) {
+  (void)hipMemsetAsync(out, 0, sizeof(double), s);
+  if (L.rows <= 0) return;
+  if (dt == DType::F64)
+    hipLaunchKernelGGL(generate_norm_kernel<double>, dim3((unsigned)L.rows), dim3(256), 0, s,
+                       static_cast<double*>(X), L.npad, L.n, L.m, L.p, L.k, kind, seed, out);
+  else
+    hipLaunchKernelGGL(generate_norm_kernel<float>, dim3((unsigned)L.rows), dim3(256), 0, s,
+                       static_cast<float*>(X), L.npad, L.n, L.m, L.p, L.k, kind, seed, out);
+}
+
 void generate(DType dt, void* X, const Layout& L, int kind, uint64_t seed, hipStream_t s) {
   const int64_t total = L.rows * L.npad;
   if (total <= 0) return;

@@ -206,6 +206,10 @@ void HipDevice::generate(DType dt, void* X, const Layout& L, GenSpec g, int s) {
   kern::generate(dt, X, L, (int)g.kind, g.seed, hs(streams_[s]));
   check_launch();
 }
+void HipDevice::generate_norm(DType dt, void* X, const Layout& L, GenSpec g, double* out, int s) {
+  kern::generate_norm(dt, X, L, (int)g.kind, g.seed, out, hs(streams_[s]));
+  check_launch();
+}
 void HipDevice::widen(DType dt, double* dst, int64_t ldd, const void* X, int64_t ldx, int64_t rows,
                       int64_t cols, int s) {
   kern::widen(dt, dst, ldd, X, ldx, rows, cols, hs(streams_[s]));
