@@ -523,16 +523,17 @@ __global__ __launch_bounds__(256) void permute_kernel(T* __restrict__ dst, int64
   const int64_t b = row / m, r = row - b * m;
   T* d = dst + ((int64_t)dst_blk[b] * m + r) * ldd;
   const T* s = X + row * ldx;
-  for (int64_t col = (int64_t)blockIdx.y * 1024 + threadIdx.x; col < ncols;
-       col += (int64_t)gridDim.y * 1024) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t cc = col + u * 256;
-      if (cc < ncols) {
-        const int c = (int)(cc / m), j = (int)(cc - (int64_t)c * m);
-        d[cc] = s[(int64_t)colsrc[c] * m + j];
-      }
-    }
+  // whole column blocks per iteration (no per-element index division): block c of the output row is
+  // block colsrc[c] of the input row, m contiguous elements each
+  const int64_t nb = ncols / m;
+  const int per = 256 / m > 0 ? 256 / m : 1;  // column blocks handled together by the 256 threads
+  const int lb = (int)threadIdx.x / m, jj = (int)threadIdx.x - lb * m;
+  if (m <= 256) {
+    for (int64_t c = (int64_t)blockIdx.y * per + lb; c < nb; c += (int64_t)gridDim.y * per)
+      if (lb < per) d[c * m + jj] = s[(int64_t)colsrc[c] * m + jj];
+  } else {
+    for (int64_t c = blockIdx.y; c < nb; c += gridDim.y)
+      for (int j = threadIdx.x; j < m; j += 256) d[c * m + j] = s[(int64_t)colsrc[c] * m + j];
   }
 }
 
@@ -541,7 +542,8 @@ void permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx
                     hipStream_t s) {
   if (nblk <= 0) return;
   const int64_t ncols = Nr * m;
-  const unsigned gy = (unsigned)std::min<int64_t>((ncols + 1023) / 1024, 64);
+  const int64_t per = std::max<int64_t>(1, 256 / m);
+  const unsigned gy = (unsigned)std::min<int64_t>((Nr + per * 4 - 1) / (per * 4), 64);
   dim3 grid((unsigned)(nblk * m), gy);
   if (dt == DType::F64)
     hipLaunchKernelGGL(permute_kernel<double>, grid, dim3(256), 0, s, static_cast<double*>(dst), ldd,

@@ -195,8 +195,9 @@ def _row_blocks_case(m, blocks, latency, c_in, dtype):
     assert torch.equal(T[:, sel], Tf[:, sel]) and bool((T[:, ~sel] == 5.0).all())
 
 
-def test_permute_blocks():
-    m, nblk, Nr = 32, 3, 5
+@pytest.mark.parametrize("m", [32, 60, 128, 300])
+def test_permute_blocks(m):
+    nblk, Nr = 3, 5
     X = _rand((nblk * m, Nr * m), torch.float64, 9).cuda()
     dst = torch.tensor([2, 0, 1], dtype=torch.int32, device="cuda")
     colsrc = torch.tensor([4, 3, 0, 1, 2], dtype=torch.int32, device="cuda")
