@@ -143,6 +143,7 @@ struct GemmArgs {
   int nparts;
   bool latency;     // GemmExtra::latency -> CfgSmall for few-tile launches
   bool lat_wide;    // GemmExtra::lat_wide
+  bool c_overlap;   // LDS-DMA fp64 kernel: C loads overlapped with the first slices (GJ_GLDS_COVL)
   int group;        // LDS-DMA kernel: tile rows per column-walk group (1 = row-major tile order)
   void* tneg;       // GemmExtra::tneg: -C^T of the columns < tncols also written here
   int64_t ldt, tncols;
@@ -568,37 +569,44 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
   const int cvoff = (rlane * ldc + clane) * ES;
 
   acc_t acc[MI][NJ];
-  // the accumulator's input: C itself, or GemmExtra::c_in (ld ldcin)
   const int ldi = g.cin ? (int)g.ldcin : ldc;
   const __amdgpu_buffer_rsrc_t rci = g.cin ? rsrc(static_cast<const double*>(g.cin) + m0 * g.ldcin + n0) : rc;
   const int civoff = (rlane * ldi + clane) * ES;
+  // the accumulator input: C itself, or GemmExtra::c_in (ld ldcin); masked elements as 0
+  auto load_c = [&]() {
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = rlane + i * 16 + MF::rq(q);
-      const int soff = (i * 16 + MF::rq(q)) * ldi * ES;
-      bool zrow = false;
+      for (int q = 0; q < 4; ++q) {
+        const int r = rlane + i * 16 + MF::rq(q);
+        const int soff = (i * 16 + MF::rq(q)) * ldi * ES;
+        bool zrow = false;
 #pragma unroll
-      for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) zrow |= (r >= zr0[z] && r < zr1[z]);
+        for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) zrow |= (r >= zr0[z] && r < zr1[z]);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int c = clane + j * 16;
-        if (MODE == MODE_ACC) {
-          const bool ok = r < Mt && c < Nt && !zrow && !(c >= z0 && c < z1);
-          acc[i][j][q] = bload<double>(rci, ok ? civoff + j * 16 * ES : kOOB, soff);
-        } else {
-          acc[i][j][q] = 0.0;
+        for (int j = 0; j < NJ; ++j) {
+          const int c = clane + j * 16;
+          if (MODE == MODE_ACC) {
+            const bool ok = r < Mt && c < Nt && !zrow && !(c >= z0 && c < z1);
+            acc[i][j][q] = bload<double>(rci, ok ? civoff + j * 16 * ES : kOOB, soff);
+          } else {
+            acc[i][j][q] = 0.0;
+          }
         }
       }
-    }
-  // C must have landed before the first LDS-DMA is counted by the hand-written waits below
+  };
+  // g.c_overlap: the C loads go out right behind the first slices' LDS-DMA pieces and the first
+  // wait covers both (one memory latency at the tile's start instead of two); otherwise C lands
+  // before the first piece is issued, as the hand-written waits count pieces only
+  if (!(MODE == MODE_ACC && g.c_overlap)) {
+    load_c();
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
+      for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) asm volatile("" ::"v"(acc[i][j][q]));
+        for (int q = 0; q < 4; ++q) asm volatile("" ::"v"(acc[i][j][q]));
+  }
 
   // DMA piece geometry (per wave, per slice): A rows wid and wid + 4 (lane l -> columns 2l, 2l+1);
   // B rows 2 wid + (l >> 5), columns 2 (l & 31) of the swizzled image.
@@ -650,7 +658,12 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
   const int pro = nk < NS - 1 ? nk : NS - 1;  // slices issued ahead
   if constexpr (PEEL == 0) {
     for (int kt = 0; kt < pro; ++kt) issue(kt);
-    wait_pieces<PIECES>(pro - 1);  // slice 0 landed
+    if (MODE == MODE_ACC && g.c_overlap) {
+      load_c();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the first slices and C landed
+    } else {
+      wait_pieces<PIECES>(pro - 1);  // slice 0 landed
+    }
     __builtin_amdgcn_s_barrier();
     for (int kt = 0; kt < nk; ++kt) {
       if (kt + NS - 1 < nk) issue(kt + NS - 1);
@@ -673,7 +686,12 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
     const int sa_step = __builtin_amdgcn_readfirstlane(BK * lda * ES);
     const int sb_step = __builtin_amdgcn_readfirstlane(BK * ldb * ES);
     for (int kt = 0; kt < pro; ++kt) issue(kt);
-    wait_pieces<PIECES>(pro - 1);  // slice 0 landed
+    if (MODE == MODE_ACC && g.c_overlap) {
+      load_c();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the first slices and C landed
+    } else {
+      wait_pieces<PIECES>(pro - 1);  // slice 0 landed
+    }
     __builtin_amdgcn_s_barrier();
     // steady state, NS slices per trip: every slice it issues (up to kt + 2 NS - 2) is full
     int kt = 0;
@@ -752,6 +770,16 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
 // argument; default on since round 5).  32768 x 8192 x 512 alone, one box: 2 stages 63.65 -> 66.56
 // TF/s, 3 stages 61.24 -> 67.57; the N = 32768 solve 1139 -> 1114 (2 stages) -> 1092-1093 ms
 // (3 stages), two repetitions (scripts/runs/r5_ab.sh, profiles/gemm_peel_r5.md).
+// GJ_GLDS_COVL=0/1 or set_glds_covl(): GemmArgs::c_overlap (default on; profiles/gemm_peel_r5.md)
+static int g_glds_covl = -1;
+static bool glds_covl() {
+  if (g_glds_covl < 0) {
+    const char* e = getenv("GJ_GLDS_COVL");
+    g_glds_covl = e ? (std::atoi(e) != 0) : 1;
+  }
+  return g_glds_covl != 0;
+}
+void set_glds_covl(int on) { g_glds_covl = on ? 1 : 0; }
 static int g_glds_peel = -1;
 static int glds_peel() {
   if (g_glds_peel < 0) {
@@ -1207,6 +1235,7 @@ static void fill_extra(GemmArgs& a, const GemmExtra* ex) {
   for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) a.zr[z] = (ex && z < ex->nzr) ? ex->zr[z] : kNone;
   a.latency = ex ? ex->latency : false;
   a.lat_wide = ex ? ex->lat_wide : false;
+  a.c_overlap = glds_covl();
   a.tneg = ex ? ex->tneg : nullptr;
   a.ldt = ex ? ex->ldtneg : 0;
   a.tncols = (ex && ex->tneg_cols > 0) ? ex->tneg_cols : (int64_t(1) << 62);

@@ -176,6 +176,8 @@ PYBIND11_MODULE(_C, mod) {
   mod.def("set_gemm_variant", [](const std::string& v) { kern::set_gemm_variant(kern::gemm_variant_id(v.c_str())); });
   mod.def("set_glds_peel", [](bool on) { kern::set_glds_peel(on ? 1 : 0); },
           "fp64 LDS-DMA trailing-update kernel: the peeled, stage-unrolled main loop (GJ_GLDS_PEEL)");
+  mod.def("set_glds_covl", [](bool on) { kern::set_glds_covl(on ? 1 : 0); },
+          "fp64 LDS-DMA kernel: C loads overlapped with the first K slices (GJ_GLDS_COVL)");
   mod.def("set_glds_build", [](int b) { kern::set_glds_build(b); },
           "fp64 LDS-DMA trailing-update build for every launch: 23 | 25 | 33 | 43 | 1623, 0 = auto (GJ_GLDS_BUILD)");
   mod.def("set_lat_glds", [](bool on) { kern::set_lat_glds(on ? 1 : 0); },
