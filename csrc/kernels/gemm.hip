@@ -934,33 +934,38 @@ __global__ __launch_bounds__(glds32::NT, OCC) void gemm_glds_f32(GemmArgs g) {
   const int ldi = g.cin ? (int)g.ldcin : ldc;  // the accumulator's input: C or GemmExtra::c_in
   const __amdgpu_buffer_rsrc_t rci = g.cin ? rsrc(static_cast<const float*>(g.cin) + m0 * g.ldcin + n0) : rc;
   const int civoff = (rlane * ldi + clane) * ES;
+  auto load_c = [&]() {
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int dr = i * 32 + 8 * (q >> 2) + (q & 3);
-      const int r = rlane + dr;
-      bool zrow = false;
+      for (int q = 0; q < 16; ++q) {
+        const int dr = i * 32 + 8 * (q >> 2) + (q & 3);
+        const int r = rlane + dr;
+        bool zrow = false;
 #pragma unroll
-      for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) zrow |= (r >= zr0[z] && r < zr1[z]);
+        for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) zrow |= (r >= zr0[z] && r < zr1[z]);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int c = clane + j * 32;
-        if (MODE == MODE_ACC) {
-          const bool ok = r < Mt && c < Nt && !zrow && !(c >= z0 && c < z1);
-          acc[i][j][q] = bload<float>(rci, ok ? civoff + j * 32 * ES : kOOB, dr * ldi * ES);
-        } else {
-          acc[i][j][q] = 0.0f;
+        for (int j = 0; j < NJ; ++j) {
+          const int c = clane + j * 32;
+          if (MODE == MODE_ACC) {
+            const bool ok = r < Mt && c < Nt && !zrow && !(c >= z0 && c < z1);
+            acc[i][j][q] = bload<float>(rci, ok ? civoff + j * 32 * ES : kOOB, dr * ldi * ES);
+          } else {
+            acc[i][j][q] = 0.0f;
+          }
         }
       }
-    }
-  // C must have landed before the first LDS-DMA is counted by the hand-written waits below
+  };
+  // g.c_overlap: C goes out right behind the first slices' DMA pieces (as in gemm_glds_f64)
+  if (!(MODE == MODE_ACC && g.c_overlap)) {
+    load_c();
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
+      for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) asm volatile("" ::"v"(acc[i][j][q]));
+        for (int q = 0; q < 16; ++q) asm volatile("" ::"v"(acc[i][j][q]));
+  }
 
   // DMA piece (per wave): k rows 2 (wid + 4h) + (lane >> 5), floats 4 (lane & 31) .. + 3
   const int dcol = 4 * (lane & 31), drow = lane >> 5;
@@ -1015,7 +1020,12 @@ __global__ __launch_bounds__(glds32::NT, OCC) void gemm_glds_f32(GemmArgs g) {
   const int nk = (int)((g.K + BK - 1) / BK);
   const int pro = nk < NS - 1 ? nk : NS - 1;
   for (int kt = 0; kt < pro; ++kt) issue(kt);
-  wait_slices<PIECES>(pro - 1);
+  if (MODE == MODE_ACC && g.c_overlap) {
+    load_c();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the first slices and C landed
+  } else {
+    wait_slices<PIECES>(pro - 1);
+  }
   __builtin_amdgcn_s_barrier();
   int kt = 0;
   if constexpr (PEEL == 1) {
