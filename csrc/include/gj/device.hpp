@@ -49,6 +49,9 @@ struct GemmExtra {
   // latency launch of >= 1024 rows: the LDS-DMA kernel (128 x 64 tiles, 4 per CU) instead of the
   // small tile -- the pivot chain's column updates when they run on reserved CUs (Engine::lat_wide_)
   bool lat_wide = false;
+  // latency launch on CUs reserved for the chain: the register-fed small fp64 kernel (every operand
+  // fragment loaded straight into registers, two 32-deep K chunks in flight; Engine::lat_reg_)
+  bool lat_reg = false;
   // Also write the result transposed and negated, tneg[c*ldtneg + r] = -C[r][c], for the output
   // columns c < tneg_cols (0 = all): the K-major multiplier panel of the next pivot search, fused
   // into the column update that produces it (one launch fewer on the pivot chain).

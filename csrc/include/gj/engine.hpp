@@ -203,6 +203,7 @@ class Engine {
     int split = 0;                // chain / deferred split of the column updates (split_: 0, 1, 2)
     bool lat_wide = false;        // chain column updates on the LDS-DMA kernel (lat_wide_)
     bool skip_cols = false;       // one MAIN launch per chunk around the look-ahead columns (skip_cols_)
+    bool lat_reg = false;         // the chain's latency GEMMs on the register-fed kernel (lat_reg_)
     bool chunk_skip = false;      // one chunk-pass launch per step around the panel columns (chunk_skip_)
   };
   Policy policy() const;
@@ -308,6 +309,9 @@ class Engine {
   // the same for the chunk pass's normalisation GEMMs around the panel / next-panel columns
   // (follows skip_cols_; GJ_CHUNK_SKIP=0/1 overrides)
   bool chunk_skip_ = false;
+  // the chain's latency GEMMs on the register-fed small fp64 kernel (GemmExtra::lat_reg): on under
+  // a CU reservation (GJ_LAT_REG=0/1 overrides)
+  bool lat_reg_ = false;
   std::vector<char> used_local_;       // local blocks used as pivot rows so far (host copy)
   GemmExtra chain_sel_[2], defer_sel_[2];  // by panel parity; rsel_m == 0: panel without a split
   void deferred_updates(int64_t v, int stream);

@@ -143,6 +143,7 @@ struct GemmArgs {
   int nparts;
   bool latency;     // GemmExtra::latency -> CfgSmall for few-tile launches
   bool lat_wide;    // GemmExtra::lat_wide
+  bool lat_reg;     // GemmExtra::lat_reg
   bool c_overlap;   // LDS-DMA fp64 kernel: C loads overlapped with the first slices (GJ_GLDS_COVL)
   int group;        // LDS-DMA kernel: tile rows per column-walk group (1 = row-major tile order)
   void* tneg;       // GemmExtra::tneg: -C^T of the columns < tncols also written here
@@ -766,6 +767,156 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
   }
 }
 
+// ---- the pivot chain's small fp64 GEMMs (latency launches: panel pieces, look-ahead rows, column
+// updates of a few row blocks).  The register-staged small tile walks K in 16-deep slices, each a
+// global -> LDS -> MFMA round trip: 29 us for a 128 x 256 x 128 product on an idle GPU
+// (bench/lat_gemm_probe.py).  Here every operand fragment goes straight from global memory into
+// registers, a whole 32-deep K chunk per load burst and two chunks in flight (ping-pong register
+// buffers): no LDS, no barrier, one memory latency per two chunks.  128 x 32 tile, 4 waves of
+// 32 x 32 (v_mfma_f64_16x16x4, the same k order as every other kernel: bit-identical results).
+template <int MODE>
+__global__ __launch_bounds__(256, 1) void gemm_lat_f64(GemmArgs g) {
+  if (gemm_skipped(g)) return;
+  using MF = Mfma<double>;
+  using acc_t = MF::acc_t;
+  constexpr int BM = 128, BN = 32, KC = 32, NKK = KC / 4, ES = 8;
+  const int tile = xcd_remap((int)blockIdx.x, g.tiles_m * g.tiles_n);
+  const int tm = tile / g.tiles_n, tn = tile % g.tiles_n;
+  if ((int64_t)tn * BN >= g.skc0 && (int64_t)(tn + 1) * BN <= g.skc1) return;  // GemmExtra::skip_c0/c1
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int lane = (int)(threadIdx.x & 63);
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const double* A = static_cast<const double*>(g.A);
+  const double* B = static_cast<const double*>(g.B);
+  double* C = static_cast<double*>(g.C);
+  const int lda = (int)g.lda, ldb = (int)g.ldb, ldc = (int)g.ldc, Kd = (int)g.K;
+  const int Mt = (int)((g.M - m0) < BM ? (g.M - m0) : BM);
+  const int Nt = (int)((g.N - n0) < BN ? (g.N - n0) : BN);
+  const int64_t zlo = g.zc0 - n0, zhi = g.zc1 - n0;
+  const int z0 = (int)(zlo < 0 ? 0 : (zlo > BN ? BN : zlo)), z1 = (int)(zhi < 0 ? 0 : (zhi > BN ? BN : zhi));
+  int zr0[GemmExtra::kMaxZeroRows], zr1[GemmExtra::kMaxZeroRows];
+#pragma unroll
+  for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) {
+    const int64_t lo = g.zr[z] - m0, hi = g.zr[z] + g.zh - m0;
+    zr0[z] = (int)(lo < 0 ? 0 : (lo > BM ? BM : lo));
+    zr1[z] = (int)(hi < 0 ? 0 : (hi > BM ? BM : hi));
+  }
+  // accumulator rows 32 w + 16 i + rl(lane) + rq(q), columns 16 j + (lane & 15)
+  const int rbase = 32 * w + MF::rl(lane), cl = lane & 15;
+  acc_t acc[2][2];
+  {
+    const __amdgpu_buffer_rsrc_t rci = rsrc(g.cin ? static_cast<const double*>(g.cin) + m0 * g.ldcin + n0
+                                                  : static_cast<const double*>(C + m0 * g.ldc + n0));
+    const int ldi = g.cin ? (int)g.ldcin : ldc;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = rbase + 16 * i + MF::rq(q);
+        bool zrow = false;
+#pragma unroll
+        for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) zrow |= (r >= zr0[z] && r < zr1[z]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int c = 16 * j + cl;
+          if (MODE == MODE_ACC) {
+            const bool ok = r < Mt && c < Nt && !zrow && !(c >= z0 && c < z1);
+            acc[i][j][q] = bload<double>(rci, ok ? (r * ldi + c) * ES : kOOB, 0);
+          } else {
+            acc[i][j][q] = 0.0;
+          }
+        }
+      }
+  }
+  // operand fragments: A row 32 w + 16 i + (lane & 15), B column 16 j + (lane & 15), k = 4 kk + (lane >> 4)
+  const int ar = 32 * w + cl, kl = lane >> 4;
+  const bool a_ok0 = ar < Mt, a_ok1 = ar + 16 < Mt, b_ok0 = cl < Nt, b_ok1 = cl + 16 < Nt;
+  const __amdgpu_buffer_rsrc_t ra = rsrc(A + m0), rb = rsrc(B + n0);
+  double fa0[NKK][2], fb0[NKK][2], fa1[NKK][2], fb1[NKK][2];
+  auto load = [&](double (&fa)[NKK][2], double (&fb)[NKK][2], int k0) {
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {
+      const int k = k0 + 4 * kk + kl;
+      const bool kok = k < Kd;
+      fa[kk][0] = bload<double>(ra, (kok && a_ok0) ? (k * lda + ar) * ES : kOOB, 0);
+      fa[kk][1] = bload<double>(ra, (kok && a_ok1) ? (k * lda + ar + 16) * ES : kOOB, 0);
+      fb[kk][0] = bload<double>(rb, (kok && b_ok0) ? (k * ldb + cl) * ES : kOOB, 0);
+      fb[kk][1] = bload<double>(rb, (kok && b_ok1) ? (k * ldb + cl + 16) * ES : kOOB, 0);
+    }
+  };
+  auto compute = [&](const double (&fa)[NKK][2], const double (&fb)[NKK][2]) {
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = MF::op(fa[kk][i], fb[kk][j], acc[i][j]);
+  };
+  const int nch = (Kd + KC - 1) / KC;
+  if (nch > 0) load(fa0, fb0, 0);
+  if (nch > 1) load(fa1, fb1, KC);
+  for (int c = 0; c < nch; c += 2) {
+    compute(fa0, fb0);
+    if (c + 2 < nch) load(fa0, fb0, (c + 2) * KC);
+    if (c + 1 < nch) {
+      compute(fa1, fb1);
+      if (c + 3 < nch) load(fa1, fb1, (c + 3) * KC);
+    }
+  }
+  const __amdgpu_buffer_rsrc_t rc = rsrc(C + m0 * g.ldc + n0);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = rbase + 16 * i + MF::rq(q);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = 16 * j + cl;
+        bstore(acc[i][j][q], rc, (r < Mt && c < Nt) ? (r * ldc + c) * ES : kOOB, 0);
+      }
+    }
+  if (g.tneg && n0 < g.tncols) {  // -C^T of the columns < tncols (GemmExtra::tneg)
+    const __amdgpu_buffer_rsrc_t rt = rsrc(static_cast<double*>(g.tneg) + n0 * g.ldt + m0);
+    const int ldt = (int)g.ldt;
+    const int Ntn = (int)((g.tncols - n0) < Nt ? (g.tncols - n0) : Nt);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = rbase + 16 * i + MF::rq(q);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int c = 16 * j + cl;
+          bstore(-acc[i][j][q], rt, (r < Mt && c < Ntn) ? (c * ldt + r) * ES : kOOB, 0);
+        }
+      }
+  }
+}
+
+// fp64 latency launches on gemm_lat_f64: per launch by GemmExtra::lat_reg (the engine sets it
+// where CUs are reserved for the chain -- without a reservation its 208-register waves wait for
+// room beside the trailing update: N = 32768 1069 -> 1096 ms), or forced for every launch by
+// GJ_LAT_KERNEL=0/1 / set_lat_kernel(0 | 1); set_lat_kernel(-1) restores the per-launch choice
+static int g_lat_kernel = -2;  // -2: not read yet, -1: per launch, 0 / 1: forced
+static bool lat_kernel(const GemmArgs& a) {
+  if (g_lat_kernel == -2) {
+    const char* e = getenv("GJ_LAT_KERNEL");
+    g_lat_kernel = e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
+  }
+  return g_lat_kernel < 0 ? a.lat_reg : g_lat_kernel != 0;
+}
+void set_lat_kernel(int mode) { g_lat_kernel = mode < 0 ? -1 : (mode != 0 ? 1 : 0); }
+
+template <int MODE>
+static void launch_lat(const GemmArgs& a0, hipStream_t s) {
+  GemmArgs a = a0;
+  a.tiles_m = (int)((a.M + 127) / 128);
+  a.tiles_n = (int)((a.N + 31) / 32);
+  const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;
+  if (nwg <= 0) return;
+  hipLaunchKernelGGL((gemm_lat_f64<MODE>), dim3((unsigned)nwg), dim3(256), 0, s, a);
+}
+
 // GJ_GLDS_PEEL=0/1 or set_glds_peel(): the peeled, stage-unrolled main loop (PEEL template
 // argument; default on since round 5).  32768 x 8192 x 512 alone, one box: 2 stages 63.65 -> 66.56
 // TF/s, 3 stages 61.24 -> 67.57; the N = 32768 solve 1139 -> 1114 (2 stages) -> 1092-1093 ms
@@ -1195,6 +1346,11 @@ static void launch(const GemmArgs& a, hipStream_t s) {
   const int64_t narrow_tiles = ((a.M + CfgNarrow::BM - 1) / CfgNarrow::BM) * ((a.N + CfgNarrow::BN - 1) / CfgNarrow::BN);
   if (a.latency && narrow_tiles < kSmallGridTiles && gemm_variant() != 0) {
     if (lat_glds(a) && a.M >= kLatGldsRows && gemm_variant() == kAutoVariant && try_glds<T, AL, MODE>(a, s)) return;
+    if constexpr (sizeof(T) == 8 && AL == 1 && MODE != MODE_RESID) {
+      if (lat_kernel(a) && gemm_variant() == kAutoVariant && a.lda * a.K * 8 < kRecords && a.ldb * a.K * 8 < kRecords &&
+          a.ldc * 128 * 8 < kRecords && (!a.cin || a.ldcin * 128 * 8 < kRecords))
+        return launch_lat<MODE>(a, s);
+    }
     return launch_cfg<T, AL, MODE, CfgSmall>(a, s);
   }
   // C_in (the chunk pass's normalisation input): the LDS-DMA kernels take it too since round 5 --
@@ -1245,6 +1401,7 @@ static void fill_extra(GemmArgs& a, const GemmExtra* ex) {
   for (int z = 0; z < GemmExtra::kMaxZeroRows; ++z) a.zr[z] = (ex && z < ex->nzr) ? ex->zr[z] : kNone;
   a.latency = ex ? ex->latency : false;
   a.lat_wide = ex ? ex->lat_wide : false;
+  a.lat_reg = ex ? ex->lat_reg : false;
   a.c_overlap = glds_covl();
   a.tneg = ex ? ex->tneg : nullptr;
   a.ldt = ex ? ex->ldtneg : 0;

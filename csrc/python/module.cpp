@@ -180,6 +180,9 @@ PYBIND11_MODULE(_C, mod) {
           "fp64 LDS-DMA kernel: C loads overlapped with the first K slices (GJ_GLDS_COVL)");
   mod.def("set_glds_build", [](int b) { kern::set_glds_build(b); },
           "fp64 LDS-DMA trailing-update build for every launch: 23 | 25 | 33 | 43 | 1623, 0 = auto (GJ_GLDS_BUILD)");
+  mod.def("set_lat_kernel", [](int mode) { kern::set_lat_kernel(mode); },
+          "fp64 latency GEMMs on the register-fed small kernel: 1 / 0 for every launch, -1 per launch "
+          "(GemmExtra::lat_reg; GJ_LAT_KERNEL)");
   mod.def("set_lat_glds", [](bool on) { kern::set_lat_glds(on ? 1 : 0); },
           "every latency GEMM of >= 1024 rows on the LDS-DMA kernel (tests; the engine sets it per launch)");
 
@@ -476,6 +479,7 @@ PYBIND11_MODULE(_C, mod) {
                                d["split"] = pl.split;
                                d["lat_wide"] = pl.lat_wide;
                                d["skip_cols"] = pl.skip_cols;
+                               d["lat_reg"] = pl.lat_reg;
                                d["chunk_skip"] = pl.chunk_skip;
                                d["bcast"] = e.eng->bcast_algo();
                                d["bcast_tuning"] = e.comm->bcast_report();

@@ -240,6 +240,11 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   skip_cols_ = reserved_cus_ > 0;
   if (const char* e = std::getenv("GJ_SKIP_COLS")) skip_cols_ = std::atoi(e) != 0;
   chunk_skip_ = skip_cols_;
+  // the chain's latency GEMMs on the register-fed small kernel where CUs are reserved for it
+  // (scripts/runs/r5_latk.sh): N = 8192 23.42 -> 22.80 ms, emulated p = 8 at N = 32768 -1.5 / -3.7 %
+  // (comm-free / direct 50 GB/s), p = 4 at N = 16384 -4 %; N = 16384 even
+  lat_reg_ = reserved_cus_ > 0;
+  if (const char* e = std::getenv("GJ_LAT_REG")) lat_reg_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("GJ_CHUNK_SKIP")) chunk_skip_ = std::atoi(e) != 0;
   lat_wide_ = reserved_cus_ > 0 && L_.p == 1;
   if (const char* e = std::getenv("GJ_LAT_GLDS")) lat_wide_ = std::atoi(e) != 0;
@@ -273,6 +278,7 @@ Engine::Policy Engine::policy() const {
   p.split = split_;
   p.lat_wide = lat_wide_;
   p.skip_cols = skip_cols_;
+  p.lat_reg = lat_reg_;
   p.chunk_skip = chunk_skip_;
   return p;
 }
@@ -781,6 +787,7 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
         GemmExtra ex = chain_sel_[par];
         ex.latency = true;
         ex.lat_wide = lat_wide_;
+        ex.lat_reg = lat_reg_;
         ex.tneg = Lt;
         ex.ldtneg = rows;
         const int64_t M = ex.rsel_m > 0 ? ex.rsel_count() * m : rows;
@@ -833,6 +840,7 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
     void* pp = elem(PP_[par], j * m * dm);
     GemmExtra lat;
     lat.latency = true;
+    lat.lat_reg = lat_reg_;
     if (ahead && L_.p > 1) {  // enqueued on every rank, executed by the pivot's owner only
       lat.owner_phys = seq_ + t;
       lat.owner_p = L_.p;
@@ -957,6 +965,7 @@ void Engine::lookahead_rows(int64_t v, bool wait_main) {
     };
     GemmExtra lat;
     lat.latency = true;
+    lat.lat_reg = lat_reg_;
     for (int64_t j = 0; j < q; ++j) {
       const PivotResult& r = piv_[par][j];
       char* seg = elem(LA_[par], j * m * wla);
@@ -1142,6 +1151,7 @@ void Engine::deferred_updates(int64_t v, int stream) {
     GemmExtra ec = sel;
     ec.latency = true;
     ec.lat_wide = lat_wide_;
+    ec.lat_reg = lat_reg_;
     ec.tneg = elem(At_[v % 3], j * m * rows);
     ec.ldtneg = rows;
     dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, M, m, j * m, At_[v % 3], rows, elem(PP_[par], j * m), dm,

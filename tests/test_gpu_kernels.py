@@ -590,3 +590,41 @@ def test_gemm_skip_columns(dtype, variant, latency, native):
         assert torch.equal(T, Tf)
     with pytest.raises(Exception, match="multiples of 128"):
         ops.gemm(A, B, C.clone(), op="acc", a_kmajor=True, skip_cols=(64, 128))
+
+
+@pytest.mark.parametrize("shape", [(128, 256, 128), (128, 512, 384), (100, 70, 100), (2048, 128, 256), (128, 96, 5)])
+@pytest.mark.parametrize("op", ["acc", "store"])
+@pytest.mark.parametrize("extras", ["none", "cin", "tneg", "masks"])
+def test_latency_kernel_bit_identical(shape, op, extras, native):
+    """gemm_lat_f64 (the register-fed small kernel of the pivot chain's latency launches) against the
+    register-staged small tile it replaces: the same products in the same k order, bit for bit,
+    including C_in, -C^T, zero row blocks / columns, ragged edges and K not a multiple of 32."""
+    M, N, K = shape
+    if extras == "cin" and op == "store":
+        pytest.skip("C_in is an accumulate-mode input")
+    At = _rand((K, M), torch.float64, 71).cuda()
+    B = _rand((K, N), torch.float64, 72).cuda()
+    C0 = _rand((M, N), torch.float64, 73).cuda()
+    kw = {}
+    if extras == "cin":
+        kw["c_in"] = _rand((M, N), torch.float64, 74).cuda()
+    if extras == "masks":
+        kw["zero_cols"] = (min(16, N), min(48, N))
+        kw["zero_rows"] = (32,)
+        kw["zero_row_height"] = 16
+    out = []
+    for on in (0, 1):
+        native.set_lat_kernel(on)
+        try:
+            C = C0.clone()
+            T = torch.full((min(N, 64), M), 3.0, dtype=torch.float64, device="cuda") if extras == "tneg" else None
+            ops.gemm(At, B, C, op=op, a_kmajor=True, latency=True, tneg=T, **kw)
+            out.append((C, T))
+        finally:
+            native.set_lat_kernel(-1)
+    assert torch.equal(out[0][0], out[1][0])
+    if extras == "tneg":
+        assert torch.equal(out[0][1], out[1][1])
+    ref = (0 if op == "store" else (kw.get("c_in", C0)).double()) + At.t() @ B
+    if extras != "masks":
+        assert torch.allclose(out[1][0], ref, rtol=1e-12, atol=1e-10)
