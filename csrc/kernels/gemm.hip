@@ -775,12 +775,10 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
 // buffers): no LDS, no barrier, one memory latency per two chunks.  128 x 32 tile, 4 waves of
 // 32 x 32 (v_mfma_f64_16x16x4, the same k order as every other kernel: bit-identical results).
 template <int MODE>
-__global__ __launch_bounds__(256, 1) void gemm_lat_f64(GemmArgs g) {
-  if (gemm_skipped(g)) return;
+__device__ __forceinline__ void lat_tile(const GemmArgs& g, int tile) {
   using MF = Mfma<double>;
   using acc_t = MF::acc_t;
   constexpr int BM = 128, BN = 32, KC = 32, NKK = KC / 4, ES = 8;
-  const int tile = xcd_remap((int)blockIdx.x, g.tiles_m * g.tiles_n);
   const int tm = tile / g.tiles_n, tn = tile % g.tiles_n;
   if ((int64_t)tn * BN >= g.skc0 && (int64_t)(tn + 1) * BN <= g.skc1) return;  // GemmExtra::skip_c0/c1
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
@@ -890,6 +888,27 @@ __global__ __launch_bounds__(256, 1) void gemm_lat_f64(GemmArgs g) {
           bstore(-acc[i][j][q], rt, (r < Mt && c < Ntn) ? (c * ldt + r) * ES : kOOB, 0);
         }
       }
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256, 1) void gemm_lat_f64(GemmArgs g) {
+  if (gemm_skipped(g)) return;
+  lat_tile<MODE>(g, xcd_remap((int)blockIdx.x, g.tiles_m * g.tiles_n));
+}
+
+// gemm_batch_kernel with the register-fed tile (128 x 32 tiles: GemmArgs::tiles_* set for it)
+__global__ __launch_bounds__(256, 1) void gemm_lat_batch_f64(GemmBatch b) {
+  if (gemm_skipped(b.a[0])) return;
+  const int bid = (int)blockIdx.x;
+  int i = 0;
+#pragma unroll
+  for (int k = 1; k < kMaxBatch; ++k) i += (k < b.n && bid >= b.start[k]) ? 1 : 0;
+  switch (i) {  // constant-index copies, as in gemm_batch_kernel
+    case 0: lat_tile<MODE_ACC>(b.a[0], bid - b.start[0]); break;
+    case 1: lat_tile<MODE_ACC>(b.a[1], bid - b.start[1]); break;
+    case 2: lat_tile<MODE_ACC>(b.a[2], bid - b.start[2]); break;
+    default: lat_tile<MODE_ACC>(b.a[3], bid - b.start[3]); break;
   }
 }
 
@@ -1448,12 +1467,24 @@ void gemm(DType dt, int op, int a_kmajor, int64_t M, int64_t N, int64_t K, const
 
 void gemm_batch(DType dt, const GemmDesc* d, int n, hipStream_t s) {
   using CF = CfgSmall;
+  // the register-fed tile (GemmExtra::lat_reg on every product, fp64, offsets within 32 bits)
+  static const bool lat_batch = !getenv("GJ_LAT_BATCH") || std::atoi(getenv("GJ_LAT_BATCH")) != 0;
+  bool lat = lat_batch && dt == DType::F64 && n > 0;
+  for (int e = 0; e < n && lat; ++e) {
+    GemmArgs t{};
+    t.lat_reg = d[e].ex.lat_reg;
+    lat = lat_kernel(t) && d[e].lda * d[e].K * 8 < kRecords && d[e].ldb * d[e].K * 8 < kRecords &&
+          d[e].ldc * 128 * 8 < kRecords;
+  }
+  const int64_t TBM = lat ? 128 : CF::BM, TBN = lat ? 32 : CF::BN;
   GemmBatch b{};
   int tiles = 0;
   auto flush = [&]() {
     if (b.n == 0) return;
     for (int k = b.n; k < kMaxBatch; ++k) b.start[k] = tiles;
-    if (dt == DType::F64)
+    if (lat)
+      hipLaunchKernelGGL(gemm_lat_batch_f64, dim3((unsigned)tiles), dim3(256), 0, s, b);
+    else if (dt == DType::F64)
       hipLaunchKernelGGL((gemm_batch_kernel<double, CF>), dim3((unsigned)tiles), dim3(CF::NT), 0, s, b);
     else
       hipLaunchKernelGGL((gemm_batch_kernel<float, CF>), dim3((unsigned)tiles), dim3(CF::NT), 0, s, b);
@@ -1472,8 +1503,8 @@ void gemm_batch(DType dt, const GemmDesc* d, int n, hipStream_t s) {
       a.zc0 = 0;
       a.zc1 = g.N;
     }
-    a.tiles_m = (int)((g.M + CF::BM - 1) / CF::BM);
-    a.tiles_n = (int)((g.N + CF::BN - 1) / CF::BN);
+    a.tiles_m = (int)((g.M + TBM - 1) / TBM);
+    a.tiles_n = (int)((g.N + TBN - 1) / TBN);
     b.start[b.n++] = tiles;
     tiles += a.tiles_m * a.tiles_n;
     if (b.n == kMaxBatch) flush();

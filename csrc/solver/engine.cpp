@@ -872,6 +872,7 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
         }
       }
       for (int i = 0; i < np; ++i) {
+        pr[i].ex.lat_reg = lat_reg_;
         pr[i].ex.owner_phys = lat.owner_phys;
         pr[i].ex.owner_p = lat.owner_p;
         pr[i].ex.owner_k = lat.owner_k;

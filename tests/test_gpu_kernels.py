@@ -628,3 +628,26 @@ def test_latency_kernel_bit_identical(shape, op, extras, native):
     ref = (0 if op == "store" else (kw.get("c_in", C0)).double()) + At.t() @ B
     if extras != "masks":
         assert torch.allclose(out[1][0], ref, rtol=1e-12, atol=1e-10)
+
+
+def test_latency_batch_kernel_bit_identical(native):
+    """gemm_batch on the register-fed tile (GemmExtra::lat_reg) against the small-tile batch: the
+    panel-piece products of one pivot step (Store blocks of different K, an Acc block), bit for bit."""
+    m = 128
+    PP = _rand((3 * m, 4 * m), torch.float64, 81).cuda()
+    L = _rand((3 * m, m), torch.float64, 82).cuda()
+    out = []
+    for on in (0, 1):
+        native.set_lat_kernel(on)
+        try:
+            RP = _rand((m, 4 * m), torch.float64, 83).cuda()
+            prods = [("store", L[0:3 * m], PP[0:3 * m, 0:m], RP[:, 0:m]),
+                     ("store", L[m:3 * m], PP[m:3 * m, m:2 * m], RP[:, m:2 * m]),
+                     ("acc", L[0:3 * m], PP[0:3 * m, 3 * m:4 * m], RP[:, 3 * m:4 * m])]
+            ops.gemm_batch(prods)
+            out.append(RP)
+        finally:
+            native.set_lat_kernel(-1)
+    assert torch.equal(out[0], out[1])
+    ref = L[0:3 * m].t() @ PP[0:3 * m, 0:m]
+    assert torch.allclose(out[1][:, 0:m], ref, rtol=1e-12, atol=1e-10)
