@@ -246,7 +246,10 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   lat_reg_ = reserved_cus_ > 0;
   if (const char* e = std::getenv("GJ_LAT_REG")) lat_reg_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("GJ_CHUNK_SKIP")) chunk_skip_ = std::atoi(e) != 0;
-  lat_wide_ = reserved_cus_ > 0 && L_.p == 1;
+  // (N = 16384, once the register-fed latency kernel exists: that kernel is 0.25 % faster for the
+  // 16384-row column update, 149.4 -> 149.0 ms; N = 8192 keeps the LDS-DMA kernel, 22.83 vs 22.92 ms;
+  // scripts/runs/r5_colupd.sh)
+  lat_wide_ = reserved_cus_ > 0 && L_.p == 1 && L_.npad <= 8192;
   if (const char* e = std::getenv("GJ_LAT_GLDS")) lat_wide_ = std::atoi(e) != 0;
   split_ = 0;
   if (const char* e = std::getenv("GJ_SPLIT")) {
