@@ -407,24 +407,27 @@ __global__ __launch_bounds__(256) void owner_edits_kernel(T* At, int64_t ldl, co
   if (g < 0 || g % p != k) return;
   const int64_t b = g / p, row0 = b * m;
   const T* inv_blk = inv + b * m * m;
-  const int64_t nrow = (j + 1) * m, total = nrow * m;
-  const int64_t e1 = total + m * m, e2 = e1 + m * mv.w, e3 = e2 + (mv.eye ? m * m : 0);
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < e3; e += (int64_t)gridDim.x * blockDim.x) {
+  // the flat index space in 32 bits (every section is far below 2^31 elements): a 32-bit division
+  // per element instead of the 64-bit division routine (the pivot chain waits for this launch)
+  const uint32_t mu = (uint32_t)m, wu = (uint32_t)(mv.w > 0 ? mv.w : 1), jm = (uint32_t)(j * m);
+  const uint32_t total = (uint32_t)((j + 1) * m * m), e1 = total + mu * mu, e2 = e1 + mu * (uint32_t)mv.w,
+                 e3 = e2 + (mv.eye ? mu * mu : 0u);
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < e3; e += gridDim.x * blockDim.x) {
     if (e < total) {
-      const int64_t kk = e / m, c = e - kk * m;
-      T* x = At + kk * ldl + row0 + c;
-      if (kk < j * m) lrow[kk * m + c] = *x;
-      *x = (kk - j * m == c) ? T(1) : T(0);
+      const uint32_t kk = e / mu, c = e - kk * mu;
+      T* x = At + (int64_t)kk * ldl + row0 + c;
+      if (kk < jm) lrow[e] = *x;  // lrow[kk * m + c]
+      *x = (kk - jm == c) ? T(1) : T(0);
     } else if (e < e1) {
       ht[e - total] = inv_blk[e - total];
     } else if (e < e2) {
-      const int64_t r = (e - e1) / mv.w, c = (e - e1) - r * mv.w;
+      const uint32_t r = (e - e1) / wu, c = (e - e1) - r * wu;
       T* x = static_cast<T*>(mv.X) + (row0 + r) * mv.ldx + mv.col0 + c;
-      static_cast<T*>(mv.dst)[r * mv.ldd + c] = *x;
+      static_cast<T*>(mv.dst)[(int64_t)r * mv.ldd + c] = *x;
       *x = T(0);
     } else {
-      const int64_t r = (e - e2) / m, c = (e - e2) - r * m;
-      static_cast<T*>(mv.eye)[r * mv.ld_eye + c] = (r == c) ? T(1) : T(0);
+      const uint32_t r = (e - e2) / mu, c = (e - e2) - r * mu;
+      static_cast<T*>(mv.eye)[(int64_t)r * mv.ld_eye + c] = (r == c) ? T(1) : T(0);
     }
   }
 }
