@@ -94,6 +94,7 @@ struct PivotSelectArgs {
   PivotResult* out = nullptr;       // p == 1 only
   PivotResult* host_out = nullptr;  // p == 1 only
   int32_t single = 0;               // 1: p == 1, the full selection
+  int32_t sysfence = 0;             // host_out publication: 1 = system-scope fences (set by the launcher)
 };
 
 }  // namespace gj

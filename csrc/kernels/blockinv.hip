@@ -845,10 +845,12 @@ bool block_inverse_select(DType dt, const void* Lt, int64_t ldl, void* inv_t, do
                           hipStream_t s, const PivotSelectArgs& sel, int variant, void* scratch) {
   const int v = variant >= 0 ? variant : bi_variant();
   if (L.nblk <= 0) return false;
+  PivotSelectArgs sa = sel;
+  sa.sysfence = host_fence();
   if (v == 5)
-    return scratch && block_inverse_co(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, nlive, s, scratch, &sel);
+    return scratch && block_inverse_co(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, nlive, s, scratch, &sa);
   if (v != 0) return false;
-  return block_inverse_mfma(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, nlive, s, &sel);
+  return block_inverse_mfma(dt, Lt, ldl, inv_t, scores, valid, used, L, thresh, nlive, s, &sa);
 }
 
 void block_inverse(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores,

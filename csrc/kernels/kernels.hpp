@@ -91,6 +91,7 @@ void pivot_local(const double* scores, const int32_t* valid, const int32_t* used
 void pivot_select_single(const double* scores, const int32_t* valid, const Layout& L, int32_t t,
                          int32_t* pos, int32_t* phys_at, int32_t* used, int32_t* seq, PivotRec* rec,
                          PivotResult* out, PivotResult* host_out, hipStream_t s);
+int host_fence();  // GJ_HOST_FENCE (misc.hip): 1 = system-scope fences around the host pivot mirror
 void pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos, int32_t* phys_at,
                   int32_t* used, int32_t* seq, PivotResult* out, PivotResult* host_out, hipStream_t s);
 void owner_edits(DType dt, void* At, int64_t ldl, const int32_t* phys, int64_t p, int64_t k, int64_t j,

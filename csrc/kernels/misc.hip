@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "gj/gen.hpp"
 #include "kernels.hpp"
@@ -242,6 +243,16 @@ void h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t m, hipStrea
 }
 
 // ---------------------------------------------------------------- pivot selection
+// GJ_HOST_FENCE=1: publish the host's pivot mirror behind system-scope fences (the round-4 form)
+// instead of system-scope relaxed stores (pivot_select.hpp pivot_finish).
+int host_fence() {
+  static const int v = [] {
+    const char* e = std::getenv("GJ_HOST_FENCE");
+    return (e && *e) ? (std::atoi(e) != 0) : 0;
+  }();
+  return v;
+}
+
 __global__ __launch_bounds__(64) void pivot_local_kernel(const double* scores, const int32_t* valid,
                                                          const int32_t* used, const int32_t* pos,
                                                          int64_t nblk, int64_t p, int64_t k,
@@ -256,38 +267,37 @@ void pivot_local(const double* scores, const int32_t* valid, const int32_t* used
                      L.p, L.k, out);
 }
 
-__global__ void pivot_global_kernel(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos,
-                                    int32_t* phys_at, int32_t* used, int32_t* seq, PivotResult* out,
-                                    PivotResult* host_out) {
+__global__ __launch_bounds__(64) void pivot_global_kernel(const PivotRec* recs, int32_t p, int32_t t,
+                                                          int32_t* pos, int32_t* phys_at, int32_t* used,
+                                                          int32_t* seq, PivotResult* out,
+                                                          PivotResult* host_out, int sysfence) {
+  const PivotRec best = pivot_gathered_wave(recs, p);
   if (threadIdx.x != 0) return;
-  PivotRec best = pivot_invalid();
-  for (int32_t q = 0; q < p; ++q)
-    if (pivot_better(recs[q], best, p)) best = recs[q];
-  pivot_finish(best, p, t, pos, phys_at, used, seq, out, host_out);
+  pivot_finish(best, p, t, pos, phys_at, used, seq, out, host_out, sysfence);
 }
 
 // p == 1: local argmin and global book-keeping in one launch (the rank's record is the gathered set).
 __global__ __launch_bounds__(64) void pivot_select_single_kernel(
     const double* scores, const int32_t* valid, int64_t nblk, int32_t t, int32_t* pos,
     int32_t* phys_at, int32_t* used, int32_t* seq, PivotRec* rec, PivotResult* out,
-    PivotResult* host_out) {
+    PivotResult* host_out, int sysfence) {
   const PivotRec best = pivot_local_wave(scores, valid, used, pos, nblk, 1, 0);
   if (threadIdx.x != 0) return;
   *rec = best;
-  pivot_finish(best, 1, t, pos, phys_at, used, seq, out, host_out);
+  pivot_finish(best, 1, t, pos, phys_at, used, seq, out, host_out, sysfence);
 }
 
 void pivot_select_single(const double* scores, const int32_t* valid, const Layout& L, int32_t t,
                          int32_t* pos, int32_t* phys_at, int32_t* used, int32_t* seq, PivotRec* rec,
                          PivotResult* out, PivotResult* host_out, hipStream_t s) {
   hipLaunchKernelGGL(pivot_select_single_kernel, dim3(1), dim3(64), 0, s, scores, valid, L.nblk, t, pos,
-                     phys_at, used, seq, rec, out, host_out);
+                     phys_at, used, seq, rec, out, host_out, host_fence());
 }
 
 void pivot_global(const PivotRec* recs, int32_t p, int32_t t, int32_t* pos, int32_t* phys_at,
                   int32_t* used, int32_t* seq, PivotResult* out, PivotResult* host_out, hipStream_t s) {
   hipLaunchKernelGGL(pivot_global_kernel, dim3(1), dim3(64), 0, s, recs, p, t, pos, phys_at, used, seq,
-                     out, host_out);
+                     out, host_out, host_fence());
 }
 
 // ---------------------------------------------------------------- partial pivoting (--pivot partial)

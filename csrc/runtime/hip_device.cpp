@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 
 #include "../kernels/kernels.hpp"
 
@@ -132,10 +133,26 @@ void HipDevice::copy2d(void* dst, size_t dpitch, const void* src, size_t spitch,
   if (w && h) HIP_OK(hipMemcpy2DAsync(dst, dpitch, src, spitch, w, h, hipMemcpyDefault, hs(streams_[s])));
 }
 
+// Ordering events (never synchronised by the host: it waits on streams or polls pinned memory).
+// GJ_EVENT_RELEASE=device records them with a device-scope release instead of HIP's default
+// system-scope one: even at N = 8192 (profiles/host_fence_r5.md).  Dropping the release altogether
+// (hipEventDisableSystemFence) was 1.2 % faster at N = 8192 but returned a wrong inverse in the
+// p = 8 async-virtual-rank golden test, so it is not offered.
+static unsigned event_release_flags() {
+  static const unsigned f = [] {
+    const char* e = std::getenv("GJ_EVENT_RELEASE");
+    const std::string v = e ? e : "";
+    if (v == "device") return (unsigned)hipEventReleaseToDevice;
+    if (v.empty() || v == "system") return 0u;
+    throw Error(Status::BadArgs, "GJ_EVENT_RELEASE must be device or system");
+  }();
+  return f;
+}
+
 int HipDevice::create_event(bool timing) {
   activate();
   hipEvent_t e;
-  HIP_OK(hipEventCreateWithFlags(&e, timing ? hipEventDefault : hipEventDisableTiming));
+  HIP_OK(hipEventCreateWithFlags(&e, timing ? hipEventDefault : (hipEventDisableTiming | event_release_flags())));
   events_.push_back(e);
   return (int)events_.size() - 1;
 }
