@@ -318,6 +318,7 @@ class Engine {
   double norm_a_ = -1;
   double local_norm_ = 0;           // this rank's ||X||_inf part, computed by generate()
   bool local_norm_valid_ = false;   // X unchanged since generate()
+  bool step_events_ = false;  // GJ_STEP_EVENTS=1: SIDE records ev_edit_ / ev_pp_ after every step
 
   // chunk plan (block-column ranges, multiples of d_ blocks so a panel never straddles chunks)
   std::vector<int64_t> cb0_, cb1_;

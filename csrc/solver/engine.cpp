@@ -88,6 +88,7 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
     : dev_(dev), comm_(comm), opt_(opt) {
   GJ_REQUIRE(n > 0 && m > 0, "n and m must be positive");
   if (const char* e = std::getenv("GJ_VERIFY")) opt_.verify = opt_.verify || std::atoi(e) != 0;
+  if (const char* e = std::getenv("GJ_STEP_EVENTS")) step_events_ = std::atoi(e) != 0;
   L_ = Layout::make(n, m, comm.size(), comm.rank());
   GJ_REQUIRE(L_.Nr < (int64_t(1) << 31), "too many block rows");
   // auto depth: profiles/small_n_sweep.md (N=8192: depth 2 34.6 vs 35.9 ms; N=16384: 4 wins), and
@@ -777,7 +778,9 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
     if (j > 0) {
       // column t after panel v-1 (look-ahead) and steps t0..t-1 of this panel; the pivot rows of
       // those steps enter as 0 without a mask: their later panel columns were moved out (take_rows)
-      dev_.wait(S_SIDE, ev_pp_[par][j - 1]);
+      // (the piece and its broadcast are on SIDE already: program order covers them; the event of
+      // step j-1 is only recorded with GJ_STEP_EVENTS=1)
+      if (step_events_) dev_.wait(S_SIDE, ev_pp_[par][j - 1]);
       if (vparts_)  // the piece that just arrived, before its first consumer (this column update)
         vhash(v, vslot(V_PP, j - 1), elem(PP_[par], (j - 1) * m * dm), dm * (int64_t)es, dm * (int64_t)es, m,
               S_SIDE);
@@ -832,7 +835,11 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
                        mv, S_SIDE);
     }
     prof_end(PH_EDITS, pe, S_SIDE);
-    dev_.record(ev_edit_[par], S_SIDE);
+    // Only the panel's last step is waited on from another stream (MAIN: lookahead_update; COMM /
+    // MAIN: the pieces), so the earlier steps record nothing (timing even: N = 8192 22.80 vs
+    // 22.85 ms, profiles/host_fence_r5.md)
+    const bool rec = step_events_ || j + 1 == q;
+    if (rec) dev_.record(ev_edit_[par], S_SIDE);
     dbg_sync();
 
     // panel piece PP_t (m x q*m, ld dm), right behind the edits on SIDE: the next step's column
@@ -892,7 +899,7 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
       comm_.bcast_many(dev_, {BcastOp{pp, (size_t)m * dm * es, root}}, S_SIDE);
     }
     prof_end(PH_PIECES, pe, S_SIDE);
-    dev_.record(ev_pp_[par][j], S_SIDE);
+    if (rec) dev_.record(ev_pp_[par][j], S_SIDE);
     dbg_sync();
   }
   if (vparts_)  // the panel's pivot sequence as SIDE left it (every rank must agree)
