@@ -295,6 +295,19 @@ PYBIND11_MODULE(_C, mod) {
                                    (PivotRec*)rec, (PivotResult*)out, nullptr, S_MAIN);
              d.sync_stream(S_MAIN);
            })
+      // p ranks' gathered records -> winner, book-keeping, *out and the pinned host mirror (returned
+      // as (step, found, phys, owner, logical, score), read after the stream completes)
+      .def("pivot_global",
+           [](Device& d, U recs, int p, int t, U pos, U phys_at, U used, U seq, U out) {
+             auto* h = static_cast<PivotResult*>(d.alloc_pinned_coherent(sizeof(PivotResult)));
+             h->step = -1;
+             d.pivot_global((const PivotRec*)recs, (int32_t)p, (int32_t)t, (int32_t*)pos, (int32_t*)phys_at,
+                            (int32_t*)used, (int32_t*)seq, (PivotResult*)out, h, S_MAIN);
+             d.sync_stream(S_MAIN);
+             py::tuple r = py::make_tuple(h->step, h->found, h->phys, h->owner, h->logical, h->score);
+             d.release_pinned(h);
+             return r;
+           })
       // Device-side latency of the batched block inverse: `reps` back-to-back launches on one
       // stream between two timing events (no host work in between); returns microseconds per call.
       .def("time_block_inverse",

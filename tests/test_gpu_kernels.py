@@ -465,6 +465,57 @@ def test_pivot_local_many_candidates(native, p, k):
     assert _rec(rec) == best
 
 
+@pytest.mark.parametrize("p", [2, 8, 64, 130])
+def test_pivot_global_records_and_host_mirror(native, p):
+    """pivot_global (misc.hip): lane q reduces record q (p > 64: several per lane), exact score ties
+    decided by the logical position, invalid records skipped; the winner's book-keeping and the
+    pinned host mirror (relaxed system-scope stores, pivot_select.hpp) against the host rule."""
+    rng = np.random.default_rng(40 + p)
+    nr = 4 * p + 3  # block rows known to the book-keeping arrays
+    t = 2
+    logical = rng.permutation(np.arange(t, nr))[:p].astype(np.int32)  # distinct, not yet pivots
+    raw = np.zeros((p, 32), dtype=np.uint8)
+    recs = []
+    for q in range(p):
+        r = {"score": float(rng.integers(1, 4)), "logical": int(logical[q]), "phys": int(logical[q]),
+             "valid": int(rng.random() > 0.25)}
+        recs.append(r)
+        raw[q, :8] = np.frombuffer(np.float64(r["score"]).tobytes(), dtype=np.uint8)
+        raw[q, 8:24] = np.frombuffer(np.array([r["logical"], r["phys"], r["valid"], 0], dtype=np.int32).tobytes(),
+                                     dtype=np.uint8)
+    best = {"valid": 0, "score": 0.0, "logical": -1, "phys": -1}
+    for r in recs:
+        if _better(r, best, p):
+            best = r
+    dev = torch.device("cuda")
+    t_r = torch.from_numpy(raw.reshape(-1)).to(dev)
+    h_pos, h_phys = list(range(nr)), list(range(nr))
+    pos = torch.tensor(h_pos, dtype=torch.int32, device=dev)
+    phys_at = torch.tensor(h_phys, dtype=torch.int32, device=dev)
+    used = torch.zeros(nr, dtype=torch.int32, device=dev)
+    seq = torch.zeros(nr, dtype=torch.int32, device=dev)
+    out = torch.zeros(32, dtype=torch.uint8, device=dev)
+    d = ops.device_for(t_r)
+    step, found, phys, owner, lg, score = d.pivot_global(t_r.data_ptr(), p, t, pos.data_ptr(), phys_at.data_ptr(),
+                                                         used.data_ptr(), seq.data_ptr(), out.data_ptr())
+    assert step == t
+    if not best["valid"]:
+        assert (found, phys, owner, lg) == (0, -1, -1, -1) and seq.cpu()[t] == -1
+        return
+    assert (found, phys, owner, lg, score) == (1, best["phys"], best["phys"] % p, best["logical"], best["score"])
+    o = out.cpu().numpy().tobytes()
+    assert tuple(np.frombuffer(o[:16], dtype=np.int32)) == (1, phys, owner, lg)
+    assert np.frombuffer(o[16:24], dtype=np.float64)[0] == score and np.frombuffer(o[24:28], dtype=np.int32)[0] == t
+    s = best["phys"]  # pivot_commit (gj/pivot.hpp)
+    q, ls = h_phys[t], h_pos[s]
+    h_pos[q] = ls
+    h_phys[ls] = q
+    h_pos[s] = t
+    h_phys[t] = s
+    assert pos.cpu().tolist() == h_pos and phys_at.cpu().tolist() == h_phys
+    assert used.cpu().tolist()[s] == 1 and seq.cpu().tolist()[t] == s
+
+
 def test_pivot_select_single_bookkeeping(native):
     m, nblk = 2, 150
     rng = np.random.default_rng(5)
