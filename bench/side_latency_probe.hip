@@ -51,6 +51,18 @@ __global__ __launch_bounds__(256) void stream_rw(double* __restrict__ b, size_t 
     for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) b[e] = b[e] * 0.999 + 1e-3;
 }
 
+// Occupancy hog: 96 KiB of LDS per workgroup (one per CU, like the trailing update's LDS-DMA
+// tiles), an FMA loop of ~`iters` steps, then retire.
+__global__ __launch_bounds__(256) void hog(double* out, int iters) {
+  extern __shared__ double lds[];
+  double v = threadIdx.x;
+#pragma unroll 1
+  for (int i = 0; i < iters; ++i) v = __builtin_fma(v, 0.999999, 1e-9);
+  lds[threadIdx.x] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x & 1023] = lds[(threadIdx.x + 1) & 255];
+}
+
 static double median(std::vector<double> v) {
   std::sort(v.begin(), v.end());
   return v.empty() ? 0.0 : v[v.size() / 2];
@@ -104,6 +116,12 @@ int main() {
     const char* name;
     hipStream_t bg;
   } cases[] = {{"idle", nullptr}, {"stream_rw on all CUs", main_all}, {"stream_rw on 224-CU mask", main_mask}};
+  double* hog_out = nullptr;
+  CHECK(hipMalloc(&hog_out, 1024 * 8));
+  hipStream_t comm;
+  CHECK(hipStreamCreateWithPriority(&comm, hipStreamNonBlocking, hi));
+  const size_t hog_lds = 96 * 1024;
+  CHECK(hipFuncSetAttribute((const void*)hog, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hog_lds));
   for (const Case& c : cases) {
     for (int which = 0; which < 3; ++which) {
       const uint32_t* chain = which == 0 ? nullptr : which == 1 ? chain_small : chain_big;
@@ -123,6 +141,40 @@ int main() {
       const char* what = which == 0 ? "no loads" : which == 1 ? "8 MiB chain" : "1 GiB chain";
       std::printf("%-26s %-12s gap median %7.2f us | per dependent load %7.0f ns\n", c.name, what,
                   median(gap) / 1e3, which == 0 ? 0.0 : median(load));
+    }
+  }
+  // LDS-holding background: workgroups of ~`iters` FMA steps, one per CU at a time
+  struct HogCase {
+    const char* name;
+    hipStream_t bg;
+    int comm_wgs;  // extra hog workgroups on an unmasked high-priority stream (the COMM chunk pass)
+  } hogs[] = {{"hog on 224-CU mask", main_mask, 0},
+              {"hog on all CUs", main_all, 0},
+              {"hog on mask + 32 COMM wgs", main_mask, 32},
+              {"hog on mask + 256 COMM wgs", main_mask, 256}};
+  const int iters = 20000;  // ~20 us per workgroup at ~1 FMA per 4 clk per wave
+  for (const HogCase& c : hogs) {
+    for (int which = 0; which < 2; ++which) {
+      const uint32_t* chain = which == 0 ? nullptr : chain_small;
+      hipLaunchKernelGGL(hog, dim3(224 * 20), dim3(256), hog_lds, c.bg, hog_out, iters);
+      if (c.comm_wgs) hipLaunchKernelGGL(hog, dim3(c.comm_wgs * 4), dim3(256), hog_lds, comm, hog_out, iters);
+      for (int i = 0; i < kProbes; ++i)
+        hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, side, chain, (uint32_t)(i * 977u), stamps + 2 * i, sink);
+      CHECK(hipGetLastError());
+      CHECK(hipStreamSynchronize(side));
+      std::vector<unsigned long long> s(kProbes * 2);
+      CHECK(hipMemcpy(s.data(), stamps, s.size() * 8, hipMemcpyDeviceToHost));
+      CHECK(hipStreamSynchronize(c.bg));
+      CHECK(hipStreamSynchronize(comm));
+      std::vector<double> gap, load;
+      for (int i = 1; i < kProbes; ++i) {
+        gap.push_back((double)(s[2 * i] - s[2 * i - 1]) * 10.0);
+        load.push_back((double)(s[2 * i + 1] - s[2 * i]) * 10.0 / kLoads);
+      }
+      std::printf("%-26s %-12s gap median %7.2f us (p90 %7.2f) | per dependent load %7.0f ns\n", c.name,
+                  which == 0 ? "no loads" : "8 MiB chain", median(gap) / 1e3,
+                  [&] { auto g = gap; std::sort(g.begin(), g.end()); return g[g.size() * 9 / 10] / 1e3; }(),
+                  which == 0 ? 0.0 : median(load));
     }
   }
   CHECK(hipDeviceSynchronize());
