@@ -63,6 +63,38 @@ __global__ __launch_bounds__(256) void hog(double* out, int iters) {
   if (threadIdx.x == 0) out[blockIdx.x & 1023] = lds[(threadIdx.x + 1) & 255];
 }
 
+// Register hog: 256 threads whose waves keep ~126 doubles live (256 VGPRs: two waves fill a SIMD) (most of a SIMD's register file,
+// like the trailing update's accumulators), ~`iters` passes, then retire.
+__global__ __launch_bounds__(256) void vhog(double* out, int iters) {
+  double a[126];
+#pragma unroll
+  for (int k = 0; k < 126; ++k) a[k] = threadIdx.x + k;
+#pragma unroll 1
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int k = 0; k < 126; ++k) a[k] = __builtin_fma(a[k], 0.999999, 1e-9);
+  }
+  double v = 0;
+#pragma unroll
+  for (int k = 0; k < 126; ++k) v += a[k];
+  if (threadIdx.x == 0) out[blockIdx.x & 1023] = v;
+}
+
+// owner_edits-shaped probe: `gridDim.x` workgroups of 256 threads, one dependent load + store each;
+// the first start and the last end over all workgroups (vector atomics on global memory).
+__global__ __launch_bounds__(256) void wide_probe(const uint32_t* __restrict__ next, uint32_t* __restrict__ dst,
+                                                  unsigned long long* __restrict__ stamp) {
+  const unsigned long long t0 = wall_clock64();
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  dst[e] = next[e] + 1u;
+  __syncthreads();
+  const unsigned long long t1 = wall_clock64();
+  if (threadIdx.x == 0) {
+    atomicMin(stamp, t0);
+    atomicMax(stamp + 1, t1);
+  }
+}
+
 static double median(std::vector<double> v) {
   std::sort(v.begin(), v.end());
   return v.empty() ? 0.0 : v[v.size() / 2];
@@ -176,6 +208,45 @@ int main() {
                   [&] { auto g = gap; std::sort(g.begin(), g.end()); return g[g.size() * 9 / 10] / 1e3; }(),
                   which == 0 ? 0.0 : median(load));
     }
+  }
+  // register-holding background, one-wave probes and 256-workgroup probes
+  uint32_t* wdst = nullptr;
+  CHECK(hipMalloc(&wdst, 256 * 256 * 4));
+  struct VCase {
+    const char* name;
+    hipStream_t bg;
+    int comm_wgs;
+  } vhogs[] = {{"none", nullptr, 0},
+               {"vhog on 224-CU mask", main_mask, 0},
+               {"vhog on all CUs", main_all, 0},
+               {"vhog on mask + 256 COMM wgs", main_mask, 256}};
+  for (const VCase& c : vhogs) {
+    if (c.bg) hipLaunchKernelGGL(vhog, dim3(224 * 800), dim3(256), 0, c.bg, hog_out, 300);
+    if (c.comm_wgs) hipLaunchKernelGGL(vhog, dim3(c.comm_wgs * 100), dim3(256), 0, comm, hog_out, 300);
+    for (int i = 0; i < kProbes; ++i)
+      hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, side, nullptr, 0u, stamps + 2 * i, sink);
+    std::vector<unsigned long long> init(kProbes * 2);
+    for (int i = 0; i < kProbes; ++i) init[2 * i] = ~0ull, init[2 * i + 1] = 0ull;
+    unsigned long long* wst = nullptr;
+    CHECK(hipMalloc(&wst, kProbes * 2 * 8));
+    CHECK(hipMemcpy(wst, init.data(), init.size() * 8, hipMemcpyHostToDevice));
+    for (int i = 0; i < kProbes; ++i)
+      hipLaunchKernelGGL(wide_probe, dim3(256), dim3(256), 0, side, chain_small, wdst, wst + 2 * i);
+    CHECK(hipGetLastError());
+    CHECK(hipStreamSynchronize(side));
+    std::vector<unsigned long long> s(kProbes * 2), w(kProbes * 2);
+    CHECK(hipMemcpy(s.data(), stamps, s.size() * 8, hipMemcpyDeviceToHost));
+    CHECK(hipMemcpy(w.data(), wst, w.size() * 8, hipMemcpyDeviceToHost));
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipFree(wst));
+    std::vector<double> gap, wdur, wgap;
+    for (int i = 1; i < kProbes; ++i) {
+      gap.push_back((double)(s[2 * i] - s[2 * i - 1]) * 10.0);
+      wdur.push_back((double)(w[2 * i + 1] - w[2 * i]) * 10.0);
+      wgap.push_back((double)(w[2 * i] - w[2 * i - 1]) * 10.0);
+    }
+    std::printf("%-28s one-wave gap %6.2f us | 256-wg probe: first start -> last end %6.2f us, gap %6.2f us\n",
+                c.name, median(gap) / 1e3, median(wdur) / 1e3, median(wgap) / 1e3);
   }
   CHECK(hipDeviceSynchronize());
   return 0;
