@@ -105,6 +105,11 @@ struct SolveStats {
   int64_t offdiag_pivots = 0;    // steps whose pivot was not the "natural" row (needed a swap)
   int64_t pivot_fallbacks = 0;   // PivotRule::Partial: steps that needed the MinInvNorm search
   double bcast_bytes = 0;        // bytes of pivot rows broadcast by this rank (as root)
+  // payload bytes of the collectives this rank took part in (p > 1), by kind: the algorithm
+  // bandwidth is bytes / the phase time of that kind (bench.py "comm_bandwidth")
+  enum CommKind : int { CK_ROWS = 0, CK_PIECES, CK_RECORDS, kNumCommKinds };
+  double comm_bytes[kNumCommKinds] = {};
+  int64_t comm_calls[kNumCommKinds] = {};
   bool profiled = false;
   double phase_ms[kNumPhases] = {};   // SolveOptions::profile only
   int64_t phase_calls[kNumPhases] = {};
@@ -143,7 +148,13 @@ class Engine {
   // parses only its own rows.  Returns Ok, CannotOpen or CannotRead (the same on every rank).
   Status load_file(const std::string& path, int nthreads = 0);
   // The input panel as it is right now (dtype elements, ld npad, layout().rows rows).
-  void* input_panel() { return X_; }
+  // A raw pointer into X: whoever writes through it changes the input behind generate()'s cached
+  // row norm, so handing it out drops that cache (a stale ||A|| in the singular test).
+  void* input_panel() {
+    local_norm_valid_ = false;
+    solved_ = false;
+    return X_;
+  }
   double norm_inf();  // collective
 
   // ---- solve (collective) ----
@@ -200,6 +211,9 @@ class Engine {
     bool la_side = true;          // look-ahead rows on SIDE (else COMM)
     std::string pivot;            // "block-min-inv-norm" | "partial"
     std::string fault_injection;  // active GJ_TEST_* knobs ("" in every normal run)
+    // every GJ_* variable set in this process's environment when the engine was built ("NAME=value"):
+    // a stray schedule override is visible in every record
+    std::vector<std::string> env_overrides;
     int split = 0;                // chain / deferred split of the column updates (split_: 0, 1, 2)
     bool lat_wide = false;        // chain column updates on the LDS-DMA kernel (lat_wide_)
     bool skip_cols = false;       // one MAIN launch per chunk around the look-ahead columns (skip_cols_)
@@ -245,13 +259,30 @@ class Engine {
   SolveStats solve_steps();
   RhsResult solve_rhs_impl(const double* b, double* x, const GenSpec* gen, const double* host_rows,
                            const void* dev_rows, int64_t ld, int max_refine, double tol);
-  // GJ_VERIFY (SolveOptions::verify): hash slots of a panel, (d*C + 3d + 1) of them:
+  // GJ_VERIFY (SolveOptions::verify): hash slots of a panel, (d*C + 3d + 1) + 3 (2d + 2) of them:
   //   [chunk c][step j] Rb segment at MAIN's chunk update | pp[j] panel piece at its first consumer
   //   | la[j] look-ahead row segment at the look-ahead update | recs[j] gathered pivot records |
   //   seq (the panel's pivot sequence, after its last step)
-  enum VKind { V_RB = 0, V_PP, V_LA, V_RECS, V_SEQ };
+  //   | rank-local hand-overs (round 6), per buffer group g (VLocal) at three points: P where the
+  //   producing stream (SIDE) finished writing it, C right before its consumer on another stream
+  //   reads it, E right after that consumer's last read.  C != P: the consumer read it before it was
+  //   produced (a missing wait, or a write not yet visible: the event release); E != P: it was
+  //   rewritten while the consumer still read it (a missing wait of the next writer).  Compared on
+  //   the rank itself, no root involved.
+  enum VKind { V_RB = 0, V_PP, V_LA, V_RECS, V_SEQ, V_LP, V_LC, V_LE };
+  // groups: 0 = the multiplier panel At[v % 3] (SIDE -> MAIN's trailing update), 1 = the panel pieces
+  // PP[v & 1], 2 .. 1+d = Lrow[v & 1][j], 2+d .. 1+2d = Ht[v & 1][j] (SIDE -> COMM's chunk pass)
+  int vlocal_groups() const { return 2 * d_ + 2; }
+  struct VRegion {
+    const void* base = nullptr;
+    int64_t ld = 0, width = 0, rows = 0;
+    std::string name;
+  };
+  VRegion vlocal_region(int64_t v, int g) const;
+  void vlocal_hash(int64_t v, VKind point, bool at_group, int s);  // the groups of one consumer
+  bool vlocal_on() const { return vparts_ && split_ == 0; }  // split_ moves At writes off SIDE
   int vslot(VKind k, int64_t j, int64_t c = 0) const;
-  int vslots() const { return (int)(d_ * (int64_t)cb0_.size() + 3 * d_ + 1); }
+  int vslots() const { return (int)(d_ * (int64_t)cb0_.size() + 3 * d_ + 1 + 3 * vlocal_groups()); }
   void vhash(int64_t v, int slot, const void* base, int64_t ld_bytes, int64_t width_bytes, int64_t rows, int s);
   void verify_hashes(const SolveStats& st);
   double residual_common(const void* A, bool wide);
@@ -313,6 +344,11 @@ class Engine {
   // a CU reservation (GJ_LAT_REG=0/1 overrides)
   bool lat_reg_ = false;
   std::vector<char> used_local_;       // local blocks used as pivot rows so far (host copy)
+  double comm_bytes_[SolveStats::kNumCommKinds] = {};  // per solve, -> SolveStats::comm_bytes
+  int64_t comm_calls_[SolveStats::kNumCommKinds] = {};
+  void count_comm(int kind, double bytes) {
+    if (L_.p > 1) comm_bytes_[kind] += bytes, comm_calls_[kind] += 1;
+  }
   GemmExtra chain_sel_[2], defer_sel_[2];  // by panel parity; rsel_m == 0: panel without a split
   void deferred_updates(int64_t v, int stream);
   double norm_a_ = -1;
@@ -393,8 +429,10 @@ class Engine {
   int64_t cur_step_ = -1;
   const char* cur_phase_ = "setup";
   std::string fault_injection_;  // active GJ_TEST_* knobs (announced, reported in policy())
+  std::vector<std::string> env_overrides_;  // GJ_* variables at construction (policy())
   int64_t hang_step_ = -1;  // GJ_TEST_HANG (fault injection)
   int64_t corrupt_step_ = -1;  // GJ_TEST_CORRUPT (a wrong inverse on purpose)
+  bool corrupt_unprofiled_ = false;  // ... only in solves without the phase timers
   // GJ_TEST_DROP_WAIT=<name>[,<name>]: leave out one ordering edge of the schedule (a planted
   // hazard the happens-before checker must report; tests only): "cp" the SIDE wait for the chunk
   // pass two panels back, "edit" MAIN's wait for the owner edits, "b" MAIN's wait for a chunk's

@@ -467,14 +467,18 @@ __global__ __launch_bounds__(CF::NT, CF::WAVES_PER_SIMD) void gemm_batch_kernel(
 // of every odd row swapped (element n of row k at n ^ 16(k&1)), so the four k rows read by one
 // ds_read_b64 land on distinct bank halves; the swizzle is applied to the global source address.
 // Requirements (checked by the dispatcher): K-major A, M, N, lda, ldb even, A/B 16-byte aligned.
+// Round 6: BN = 128 (2 x 2 waves of 64 x 64, 16 accumulator tiles per wave) as a template
+// option -- half the LDS fragment reads per MFMA (8 per 16 MFMAs instead of 6 per 8) and half the
+// A-slab traffic per flop; B rows are then 1 KiB, one DMA piece each, like A's
+// (profiles/gemm_tile128_r6.md).
 namespace glds {
 constexpr int BM = 128, BN = 64, NT = 256;
 constexpr int LDA = BM + 16;  // A row stride (doubles)
-template <int BK>
+template <int BK, int BN_ = BN>
 struct Geo {
-  static constexpr int SA = BK * LDA, SB = BK * BN;  // stage sizes (doubles)
+  static constexpr int SA = BK * LDA, SB = BK * BN_;  // stage sizes (doubles)
   static constexpr int STAGE = SA + SB;
-  static constexpr int PIECES = BK / 4 + BK / 8;     // LDS-DMA instructions per wave per slice
+  static constexpr int PIECES = BK / 4 + (BN_ == 128 ? BK / 4 : BK / 8);  // LDS-DMA instructions per wave per slice
 };
 }  // namespace glds
 
@@ -501,18 +505,11 @@ __device__ __forceinline__ void static_for(F&& f) {
 
 template <int P>
 __device__ __forceinline__ void wait_pieces(int n) {
-  static_assert(P == 3 || P == 6, "pieces per slice");
-  if (n <= 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  } else if constexpr (P == 3) {
-    if (n == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-    else if (n == 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-  } else {
-    if (n == 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else if (n == 2) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
-  }
+  static_assert(P >= 1 && 3 * P < 64, "pieces per slice");
+  if (n <= 0) wait_vm<0>();
+  else if (n == 1) wait_vm<P>();
+  else if (n == 2) wait_vm<2 * P>();
+  else wait_vm<3 * P>();
 }
 
 // PEEL = 1: the steady-state loop is unrolled over the NS stages (every LDS stage base, fragment
@@ -520,16 +517,21 @@ __device__ __forceinline__ void wait_pieces(int n) {
 // slice, if any, takes the masked issue), and each DMA piece is one per-lane offset fixed for the
 // whole launch plus the slice's byte offset in an SGPR (soffset): no per-slice VALU address or mask
 // arithmetic, and a constant vmcnt per slice.
-template <int MODE, int NS, int OCC, int BK, int PEEL = 0>
+template <int MODE, int NS, int OCC, int BK, int PEEL = 0, int BNT = glds::BN>
 __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
   using namespace glds;
   if (gemm_skipped(g)) return;
   static_assert(NS >= 2 && NS <= 5, "stages");
   static_assert(BK == 8 || BK == 16, "slice depth");
-  constexpr int SA = Geo<BK>::SA, STAGE = Geo<BK>::STAGE, PIECES = Geo<BK>::PIECES;
+  static_assert(BNT == 64 || BNT == 128, "tile width");
+  constexpr int BN = BNT;  // (shadows glds::BN)
+  constexpr int SA = Geo<BK, BN>::SA, STAGE = Geo<BK, BN>::STAGE, PIECES = Geo<BK, BN>::PIECES;
   using MF = Mfma<double>;
   using acc_t = MF::acc_t;
-  constexpr int ES = 8, TM = 64, TN = 32, MI = 4, NJ = 2, WN = 2;
+  constexpr int ES = 8, TM = 64, TN = BN / 2, MI = 4, NJ = TN / 16, WN = 2;
+  // B DMA pieces per wave per slice: BN = 64 two k rows per piece (lane >> 5 picks the row), BN = 128
+  // one k row per piece (like A)
+  constexpr int BPW = BN == 128 ? BK / 4 : BK / 8;
   __shared__ double lds[NS * STAGE];
 
   const int nwg = g.tiles_m * g.tiles_n;
@@ -610,13 +612,17 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
   }
 
   // DMA piece geometry (per wave, per slice): A rows wid and wid + 4 (lane l -> columns 2l, 2l+1);
-  // B rows 2 wid + (l >> 5), columns 2 (l & 31) of the swizzled image.
+  // BN = 64: B rows 2 wid + (l >> 5), columns 2 (l & 31) of the swizzled image; BN = 128: B rows
+  // wid + 4h, columns 2l of the swizzled image (row parity = wid's, as 4h is even).  h-th piece's
+  // LDS row: bldsrow(h).
   const int acol = 2 * lane;
   const bool a_ok = (m0L + acol) < g.M;
-  const int brow = 2 * wid + (lane >> 5);
-  const int bpos = 2 * (lane & 31);
+  const int brow = BN == 128 ? wid : 2 * wid + (lane >> 5);
+  const int bpos = BN == 128 ? 2 * lane : 2 * (lane & 31);
   const int bcol = bpos ^ ((brow & 1) * 16);
   const bool b_ok = (n0 + bcol) < g.N;
+  auto brow_h = [&](int h) { return BN == 128 ? brow + 4 * h : brow + 8 * h; };       // global k row
+  auto blds_h = [&](int h) { return BN == 128 ? (wid + 4 * h) * BN : 2 * (wid + 4 * h) * BN; };  // LDS offset
   __amdgpu_buffer_rsrc_t ra = rsrc(A + m0);
   __amdgpu_buffer_rsrc_t rb = rsrc(B + n0);
   const int Kd = (int)g.K;
@@ -630,10 +636,10 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
       dma16(ra, st + kr * LDA, ok ? ((k0 + kr) * lda + acol) * ES : kOOB);
     }
 #pragma unroll
-    for (int h = 0; h < BK / 8; ++h) {  // B rows 2 (wid + 4h) + (lane >> 5)
-      const int br = brow + 8 * h;
+    for (int h = 0; h < BPW; ++h) {
+      const int br = brow_h(h);
       const bool okb = b_ok && (k0 + br) < Kd;
-      dma16(rb, st + SA + 2 * (wid + 4 * h) * BN, okb ? ((k0 + br) * ldb + bcol) * ES : kOOB);
+      dma16(rb, st + SA + blds_h(h), okb ? ((k0 + br) * ldb + bcol) * ES : kOOB);
     }
   };
   auto compute = [&](int kt) {
@@ -679,11 +685,11 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
     }
   } else {
     const int nfull = Kd / BK;  // slices without a K mask
-    int va[BK / 4], vb[BK / 8];
+    int va[BK / 4], vb[BPW];
 #pragma unroll
     for (int h = 0; h < BK / 4; ++h) va[h] = a_ok ? ((wid + 4 * h) * lda + acol) * ES : kOOB;
 #pragma unroll
-    for (int h = 0; h < BK / 8; ++h) vb[h] = b_ok ? ((brow + 8 * h) * ldb + bcol) * ES : kOOB;
+    for (int h = 0; h < BPW; ++h) vb[h] = b_ok ? (brow_h(h) * ldb + bcol) * ES : kOOB;
     const int sa_step = __builtin_amdgcn_readfirstlane(BK * lda * ES);
     const int sb_step = __builtin_amdgcn_readfirstlane(BK * ldb * ES);
     for (int kt = 0; kt < pro; ++kt) issue(kt);
@@ -704,7 +710,7 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
 #pragma unroll
         for (int h = 0; h < BK / 4; ++h) dma16(ra, st + (wid + 4 * h) * LDA, va[h], kn * sa_step);
 #pragma unroll
-        for (int h = 0; h < BK / 8; ++h) dma16(rb, st + SA + 2 * (wid + 4 * h) * BN, vb[h], kn * sb_step);
+        for (int h = 0; h < BPW; ++h) dma16(rb, st + SA + blds_h(h), vb[h], kn * sb_step);
         const double* sa = lds + S0 * STAGE;
         const double* sb = sa + SA;
 #pragma unroll
@@ -967,20 +973,54 @@ static int glds_build_forced() {
     const char* e = getenv("GJ_GLDS_BUILD");
     const std::string v = e ? e : "";
     g_glds_build = v.empty() ? 0 : v == "2.5" ? 25 : v == "3.3" ? 33 : v == "2.3" ? 23 : v == "4.3" ? 43
-                                                  : v == "16.2.3" ? 1623 : -2;
-    if (g_glds_build == -2) throw std::invalid_argument("GJ_GLDS_BUILD: 2.3 | 2.5 | 3.3 | 4.3 | 16.2.3");
+                                                  : v == "16.2.3" ? 1623 : v == "3.2" ? 32 : -2;
+    if (g_glds_build == -2) throw std::invalid_argument("GJ_GLDS_BUILD: 2.3 | 2.5 | 3.3 | 4.3 | 16.2.3 | 3.2");
   }
   return g_glds_build;
 }
 void set_glds_build(int b) {
-  if (b != 0 && b != 23 && b != 25 && b != 33 && b != 43 && b != 1623)
-    throw std::invalid_argument("glds build: 0 | 23 | 25 | 33 | 43 | 1623");
+  if (b != 0 && b != 23 && b != 25 && b != 33 && b != 43 && b != 1623 && b != 32)
+    throw std::invalid_argument("glds build: 0 | 23 | 25 | 32 | 33 | 43 | 1623");
   g_glds_build = b;
+}
+
+// GJ_GLDS_TILE=64|128 or set_glds_tile(): the LDS-DMA kernel's tile width (BN) for the launches
+// that take the 4-per-CU builds (the 5-per-CU dense build stays 128 x 64); profiles/gemm_tile128_r6.md
+static int g_glds_tile = -1;
+static int glds_tile() {
+  if (g_glds_tile < 0) {
+    const char* e = getenv("GJ_GLDS_TILE");
+    const int v = e ? std::atoi(e) : 64;
+    if (v != 64 && v != 128) throw std::invalid_argument("GJ_GLDS_TILE: 64 | 128");
+    g_glds_tile = v;
+  }
+  return g_glds_tile;
+}
+void set_glds_tile(int bn) {
+  if (bn != 64 && bn != 128) throw std::invalid_argument("glds tile: 64 | 128");
+  g_glds_tile = bn;
 }
 
 template <int MODE>
 static void launch_glds(const GemmArgs& a0, hipStream_t s) {
   GemmArgs a = a0;
+  const int forced0 = glds_build_forced();
+  const int build0 = forced0 ? forced0 : a.dense ? 25 : glds_peel() ? 33 : 23;
+  if (glds_tile() == 128 && glds_peel() && build0 != 25) {
+    // 128 x 128 tiles: 16 accumulator tiles per wave (128 VGPRs); <stages, W> 3.3 / 2.3 / 3.2
+    a.tiles_m = (int)((a.M + glds::BM - 1) / glds::BM);
+    a.tiles_n = (int)((a.N + 127) / 128);
+    const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;
+    if (nwg <= 0) return;
+    a.group = 4;
+    if (build0 == 23)
+      hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 3, 8, 1, 128>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
+    else if (build0 == 32)
+      hipLaunchKernelGGL((gemm_glds_f64<MODE, 3, 2, 8, 1, 128>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
+    else
+      hipLaunchKernelGGL((gemm_glds_f64<MODE, 3, 3, 8, 1, 128>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
+    return;
+  }
   a.tiles_m = (int)((a.M + glds::BM - 1) / glds::BM);
   a.tiles_n = (int)((a.N + glds::BN - 1) / glds::BN);
   const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;

@@ -122,6 +122,17 @@ py::dict stats_to_dict(const SolveStats& st) {
   d["offdiag_pivots"] = st.offdiag_pivots;
   d["pivot_fallbacks"] = st.pivot_fallbacks;
   d["bcast_bytes"] = st.bcast_bytes;
+  {
+    static const char* kinds[SolveStats::kNumCommKinds] = {"pivot_rows", "panel_pieces", "pivot_records"};
+    py::dict cb;
+    for (int k = 0; k < SolveStats::kNumCommKinds; ++k) {
+      py::dict e;
+      e["bytes"] = st.comm_bytes[k];
+      e["calls"] = st.comm_calls[k];
+      cb[kinds[k]] = e;
+    }
+    d["comm_bytes"] = cb;
+  }
   if (st.profiled) {
     py::dict ph;
     for (int i = 0; i < kNumPhases; ++i) {
@@ -180,6 +191,8 @@ PYBIND11_MODULE(_C, mod) {
           "fp64 LDS-DMA kernel: C loads overlapped with the first K slices (GJ_GLDS_COVL)");
   mod.def("set_glds_build", [](int b) { kern::set_glds_build(b); },
           "fp64 LDS-DMA trailing-update build for every launch: 23 | 25 | 33 | 43 | 1623, 0 = auto (GJ_GLDS_BUILD)");
+  mod.def("set_glds_tile", [](int bn) { kern::set_glds_tile(bn); },
+          "fp64 LDS-DMA trailing-update tile width for the 4-per-CU builds: 64 | 128 (GJ_GLDS_TILE)");
   mod.def("set_lat_kernel", [](int mode) { kern::set_lat_kernel(mode); },
           "fp64 latency GEMMs on the register-fed small kernel: 1 / 0 for every launch, -1 per launch "
           "(GemmExtra::lat_reg; GJ_LAT_KERNEL)");
@@ -489,6 +502,7 @@ PYBIND11_MODULE(_C, mod) {
                                d["look_ahead_rows"] = pl.la_side ? "SIDE" : "COMM";
                                d["pivot"] = pl.pivot;
                                if (!pl.fault_injection.empty()) d["fault_injection"] = pl.fault_injection;
+                               d["env_overrides"] = pl.env_overrides;
                                d["split"] = pl.split;
                                d["lat_wide"] = pl.lat_wide;
                                d["skip_cols"] = pl.skip_cols;
@@ -556,6 +570,32 @@ PYBIND11_MODULE(_C, mod) {
            py::arg("b"), py::arg("rows_f64"), py::arg("ld"), py::arg("max_refine") = -1, py::arg("tol") = 1e-15,
            "A x = b after solve(): x = inv(A) b by the native GEMV, refined in fp64 against this rank's rows "
            "of A given as an fp64 device array (Engine::solve_rhs_device); returns (x, info)")
+      .def("solve_rhs_generated",
+           [](PyEngine& e, const std::string& kind, uint64_t seed,
+              py::array_t<double, py::array::c_style | py::array::forcecast> b, int max_refine, double tol) {
+             const int64_t n = e.eng->layout().n;
+             if (b.ndim() != 1 || b.shape(0) != n) throw std::invalid_argument("b must be an n-vector");
+             if (max_refine < 0) max_refine = e.eng->options().dtype == DType::F64 ? 2 : 10;
+             GenSpec g;
+             g.kind = parse_gen(kind);
+             g.seed = seed;
+             py::array_t<double> x(n);
+             RhsResult rr;
+             {
+               py::gil_scoped_release rel;
+               rr = e.eng->solve_rhs(b.data(), x.mutable_data(), &g, nullptr, 0, max_refine, tol);
+             }
+             py::dict info;
+             info["residual"] = rr.residual;
+             info["backward_error"] = rr.backward_error;
+             info["history"] = rr.history;
+             info["steps"] = rr.steps;
+             info["converged"] = rr.converged;
+             return py::make_tuple(x, info);
+           },
+           py::arg("kind"), py::arg("seed"), py::arg("b"), py::arg("max_refine") = -1, py::arg("tol") = 1e-15,
+           "A x = b after solve() of the generated matrix (kind, seed): x = inv(A) b, refined in fp64 against A "
+           "regenerated in fp64 (Engine::solve_rhs); returns (x, info) -- BASELINE config 5 as a solve")
       .def("input_panel_ptr", [](PyEngine& e) { return (uintptr_t)e.eng->input_panel(); })
       .def("result_panel_ptr", [](PyEngine& e) { return (uintptr_t)e.eng->result_panel(); })
       .def("norm_inf", [](PyEngine& e) {

@@ -173,33 +173,55 @@ std::string Comm::tune_bcast(Device& dev, std::vector<size_t> sizes) {
     ok_local = ok_local && std::memcmp(got.data(), pat.data(), maxb) == 0;
   }
   const bool ok = host_max(dev, ok_local ? 0.0 : 1.0) == 0.0;
-  auto time_algo = [&](bool direct, size_t bytes) {
+  // One timed round = p broadcasts (every rank the root once), the max over ranks of its mean per
+  // broadcast.  The two algorithms alternate round by round (a drifting clock or a busy link hits
+  // both), kRounds rounds each after 2 warm-ups; the decision uses the MEDIANS, and the report
+  // carries median, min and max of both (2p samples decided the p = 8 pick, whose wrong
+  // choice costs 72 % under the model).
+  constexpr int kRounds = 7;
+  auto round_ms = [&](bool direct, size_t bytes) {
     auto run = [&](int it) {
       const BcastOp o{buf, bytes, it % p};
       if (direct) bcast_direct(dev, {o}, s);
       else bcast(dev, o.buf, o.bytes, o.root, s);
     };
-    for (int it = 0; it < 2; ++it) run(it);
     drain(dev, s);
     host_max(dev, 0.0);  // barrier
     const auto t0 = std::chrono::steady_clock::now();
-    const int iters = 2 * p;
-    for (int it = 0; it < iters; ++it) run(it);
+    for (int it = 0; it < p; ++it) run(it);
     drain(dev, s);
-    const double ms =
-        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / iters;
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / p;
     return host_max(dev, ms);
+  };
+  struct Stat { double med = -1, lo = -1, hi = -1; };
+  auto stat = [](std::vector<double> v) {
+    Stat r;
+    if (v.empty()) return r;
+    std::sort(v.begin(), v.end());
+    r.med = v[v.size() / 2];
+    r.lo = v.front();
+    r.hi = v.back();
+    return r;
   };
   // direct from the smallest measured size at which it wins at that and every larger size
   std::string detail;
   size_t thr = 0;
   bool wins_above = true;
   std::vector<bool> win(sizes.size());
-  std::vector<double> tr(sizes.size()), td(sizes.size());
+  std::vector<Stat> tr(sizes.size()), td(sizes.size());
   for (size_t i = 0; i < sizes.size(); ++i) {
-    tr[i] = time_algo(false, sizes[i]);
-    td[i] = ok ? time_algo(true, sizes[i]) : -1.0;
-    win[i] = ok && td[i] < 0.95 * tr[i];
+    for (int w = 0; w < 2; ++w) {  // warm-ups of both
+      round_ms(false, sizes[i]);
+      if (ok) round_ms(true, sizes[i]);
+    }
+    std::vector<double> vr, vd;
+    for (int r = 0; r < kRounds; ++r) {
+      vr.push_back(round_ms(false, sizes[i]));
+      if (ok) vd.push_back(round_ms(true, sizes[i]));
+    }
+    tr[i] = stat(vr);
+    td[i] = stat(vd);
+    win[i] = ok && td[i].med < 0.95 * tr[i].med;
   }
   for (size_t i = sizes.size(); i-- > 0;) {
     wins_above = wins_above && win[i];
@@ -208,8 +230,10 @@ std::string Comm::tune_bcast(Device& dev, std::vector<size_t> sizes) {
   dev.release(buf);
   direct_min_ = thr;
   for (size_t i = 0; i < sizes.size(); ++i) {
-    char line[128];
-    std::snprintf(line, sizeof line, "%s%zu B: ring %.3f ms, direct %.3f ms", i ? "; " : "", sizes[i], tr[i], td[i]);
+    char line[256];
+    std::snprintf(line, sizeof line,
+                  "%s%zu B: ring %.3f ms [%.3f-%.3f], direct %.3f ms [%.3f-%.3f] (median [min-max] of %d rounds)",
+                  i ? "; " : "", sizes[i], tr[i].med, tr[i].lo, tr[i].hi, td[i].med, td[i].lo, td[i].hi, kRounds);
     detail += line;
   }
   const std::string choice = thr == 0 ? "ring" : (thr == sizes.front() ? "direct" : "direct from " + std::to_string(thr) + " B");

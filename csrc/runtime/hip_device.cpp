@@ -137,14 +137,21 @@ void HipDevice::copy2d(void* dst, size_t dpitch, const void* src, size_t spitch,
 // GJ_EVENT_RELEASE=device records them with a device-scope release instead of HIP's default
 // system-scope one: even at N = 8192 (profiles/host_fence_r5.md).  Dropping the release altogether
 // (hipEventDisableSystemFence) was 1.2 % faster at N = 8192 but returned a wrong inverse in the
-// p = 8 async-virtual-rank golden test, so it is not offered.
+// p = 8 async-virtual-rank golden test: `none` exists only as fault injection, to reproduce that
+// failure under GJ_VERIFY (announced on stderr and in the engine policy's fault_injection;
+// profiles/verify_r6.md).
 static unsigned event_release_flags() {
   static const unsigned f = [] {
     const char* e = std::getenv("GJ_EVENT_RELEASE");
     const std::string v = e ? e : "";
     if (v == "device") return (unsigned)hipEventReleaseToDevice;
+    if (v == "none") {
+      std::fprintf(stderr, "gj: WARNING: FAULT INJECTION ACTIVE (GJ_EVENT_RELEASE=none): ordering events "
+                           "carry no release fence; cross-stream hand-overs may read stale data\n");
+      return (unsigned)hipEventDisableSystemFence;
+    }
     if (v.empty() || v == "system") return 0u;
-    throw Error(Status::BadArgs, "GJ_EVENT_RELEASE must be device or system");
+    throw Error(Status::BadArgs, "GJ_EVENT_RELEASE must be device or system (none: fault injection only)");
   }();
   return f;
 }

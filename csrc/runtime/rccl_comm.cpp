@@ -42,15 +42,18 @@ RcclComm::RcclComm(const std::vector<std::string>& ids, int nranks, int rank, in
   GJ_REQUIRE(ids.size() == 2, "RcclComm needs two unique ids");
   if (nranks > 1 && !one_comm_) {
     // Two concurrently active communicators need their own hardware queues (README "Progress of
-    // the two communicators").  The launchers agree on the count HIP really runs with and pick
-    // the one-communicator schedule below 16 (parallel/dist.py agree_comm_mode, cli/main.cpp);
-    // here only the environment is visible, so an embedder that constructs this directly is warned.
+    // the two communicators"): on a shared queue a SIDE kernel spinning on a peer can sit in front
+    // of the COMM kernel that peer waits for -- a cross-rank deadlock that only surfaces as a comm
+    // timeout.  The launchers agree on the count HIP really runs with and pass one_comm below 16
+    // (parallel/dist.py agree_comm_mode, cli/main.cpp); an embedder that constructs this directly
+    // with fewer queues is refused unless it opts in with GJ_ALLOW_SHARED_QUEUES=1.
     const char* q = std::getenv("GPU_MAX_HW_QUEUES");
-    if (!q || std::atoi(q) < kMinHwQueues)
-      std::fprintf(stderr,
-                   "gj: warning: two RCCL communicators with GPU_MAX_HW_QUEUES=%s < %d: they may share a "
-                   "hardware queue; pass one_comm (GJ_ONE_COMM=1) unless HIP was initialised with more\n",
-                   q ? q : "unset", kMinHwQueues);
+    const char* allow = std::getenv("GJ_ALLOW_SHARED_QUEUES");
+    if ((!q || std::atoi(q) < kMinHwQueues) && !(allow && std::atoi(allow) != 0))
+      throw Error(Status::BadArgs,
+                  std::string("two RCCL communicators need GPU_MAX_HW_QUEUES >= ") + std::to_string(kMinHwQueues) +
+                      " (have " + (q ? q : "unset") + "): pass one_comm (GJ_ONE_COMM=1), raise the queue count "
+                      "before the first HIP call, or set GJ_ALLOW_SHARED_QUEUES=1");
   }
   (void)hipSetDevice(device_);
   for (int c = 0; c < (one_comm_ ? 1 : 2); ++c) {

@@ -32,6 +32,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+
+#include <unistd.h>  // environ
 #include <thread>
 
 namespace gj {
@@ -97,17 +99,14 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // communication-cost model 0.167 vs 0.177 s, while depth 6 / 8 lose at p = 1 / 2 / 4 and at
   // N = 16384: profiles/depth_pgt1.md)
   const bool small_rank = L_.p > 1 && L_.max_nblk * L_.m <= 4096;
-  // Depth 2 also on p > 1 ranks of <= 2048 rows (p = 8 at N = 16384, p = 4 at N = 8192): 0.0382
-  // vs 0.0408 s per emulated p = 8 rank at N = 16384 under the direct 50 GB/s model
-  // (profiles/depth_pgt1.md).  It was held back after one round-3 async-virtual-rank run at p = 8,
-  // depth 2 returned a wrong inverse; round 5 re-enabled it once the GPU tier ran that
-  // configuration with consumption-point verification on (GJ_VERIFY, tests/test_gpu_engine.py
-  // test_depth2_p8_async_jittered: every broadcast buffer's bytes checked where it is consumed).
+  // Depth 2 on p > 1 ranks of <= 2048 rows (p = 8 at N = 16384) is 0.0382 vs 0.0408 s per emulated
+  // rank under the direct 50 GB/s model (profiles/depth_pgt1.md), but it is the configuration of
+  // the round-3 wrong inverse (p = 8, depth 2, async ranks), whose cause is not localised
+  // (profiles/verify_r6.md): p > 1 keeps depth 4 by default; --depth 2 selects it explicitly.
   // (One GPU at N = 32768, depth 8 with the co-resident candidate inverse: 0.9 % faster on one box,
   // 0.5-0.8 % slower on another, same-box A/Bs of round 4 -- not adopted, profiles/rocprof_n32768_r4.md.)
-  const bool tiny_rank = L_.p > 1 && L_.max_nblk * L_.m <= 2048;
   const int want = opt_.depth > 0 ? opt_.depth
-                   : ((L_.p == 1 && L_.npad <= 8192) || tiny_rank) ? 2
+                   : (L_.p == 1 && L_.npad <= 8192) ? 2
                    : (small_rank && L_.npad > 16384) ? 8 : 4;
   d_ = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)want, (int64_t)kMaxDepth, L_.Nr}));
 
@@ -174,12 +173,20 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
         if (!fault_injection_.empty()) fault_injection_ += " ";
         fault_injection_ += std::string(var) + "=" + e;
       }
+  if (const char* e = std::getenv("GJ_EVENT_RELEASE"))
+    if (std::string(e) == "none") fault_injection_ += std::string(fault_injection_.empty() ? "" : " ") + "GJ_EVENT_RELEASE=none";
   if (!fault_injection_.empty())
     std::fprintf(stderr, "gj: rank %d: WARNING: FAULT INJECTION ACTIVE (%s): results of this run are "
                          "deliberately wrong, hung or failed\n",
                  (int)L_.k, fault_injection_.c_str());
+  for (char** e = environ; e && *e; ++e)
+    if (std::strncmp(*e, "GJ_", 3) == 0) env_overrides_.push_back(*e);
+  std::sort(env_overrides_.begin(), env_overrides_.end());
   hang_step_ = injected_step("GJ_TEST_HANG", L_.k);
   corrupt_step_ = injected_step("GJ_TEST_CORRUPT", L_.k);
+  // "<rank>:<step>:unprofiled": only solves without the phase timers are corrupted (the bench's
+  // timed solves, not its untimed profiled one -- tests that the gate checks a timed solve)
+  if (const char* e = std::getenv("GJ_TEST_CORRUPT")) corrupt_unprofiled_ = std::strstr(e, ":unprofiled") != nullptr;
   if (const char* e = std::getenv("GJ_TEST_DROP_WAIT")) drop_wait_ = std::string(",") + e + ",";
   dev_.trace_context(&cur_step_, &cur_phase_);  // names the step / phase in schedule-check reports
   // Allocation, agreed on every rank BEFORE any other collective (reference main.cpp:366-381 and
@@ -270,6 +277,7 @@ Engine::~Engine() {
 Engine::Policy Engine::policy() const {
   Policy p;
   p.depth = d_;
+  p.env_overrides = env_overrides_;
   p.nchunks = (int)cb0_.size();
   for (size_t c = 0; c < cb0_.size(); ++c) p.chunk_cols = std::max(p.chunk_cols, chunk_w((int64_t)c));
   p.reserve_cus = reserved_cus_;
@@ -726,6 +734,7 @@ void Engine::select(int64_t t, const void* Lt, bool full) {
   pe = prof_begin(S_SIDE);
   comm_.set_step(t);
   if (L_.p > 1) comm_.allgather(dev_, myrec_, recs_, sizeof(PivotRec), S_SIDE);
+  count_comm(SolveStats::CK_RECORDS, double(sizeof(PivotRec)) * L_.p);
   dev_.host_access(&piv_host_[par].step, sizeof(int32_t), true);
   piv_host_[par].step = -1;
   dev_.pivot_global(L_.p > 1 ? recs_ : myrec_, (int32_t)L_.p, (int32_t)t, pos_, phys_at_, used_, seq_, piv_dev_,
@@ -898,12 +907,14 @@ bool Engine::factor_panel(int64_t v, SolveStats& st, double& host_wait) {
     } else {
       comm_.bcast_many(dev_, {BcastOp{pp, (size_t)m * dm * es, root}}, S_SIDE);
     }
+    count_comm(SolveStats::CK_PIECES, double(m) * dm * es);
     prof_end(PH_PIECES, pe, S_SIDE);
     if (rec) dev_.record(ev_pp_[par][j], S_SIDE);
     dbg_sync();
   }
   if (vparts_)  // the panel's pivot sequence as SIDE left it (every rank must agree)
     vhash(v, vslot(V_SEQ, 0), seq_ + t0, (int64_t)sizeof(int32_t) * q, (int64_t)sizeof(int32_t) * q, 1, S_SIDE);
+  if (vlocal_on()) vlocal_hash(v, V_LP, true, S_SIDE);  // what SIDE hands over to MAIN / COMM
   if (ahead) {  // the panel's pivots, in step order (the first singular step ends the solve)
     cur_phase_ = "pivot search";
     for (int64_t j = 0; j < q; ++j) {
@@ -970,6 +981,7 @@ void Engine::lookahead_rows(int64_t v, bool wait_main) {
     auto lflush = [&]() {
       if (lops.empty()) return;
       const int pb = prof_begin(ls);
+      for (const auto& o : lops) count_comm(SolveStats::CK_ROWS, (double)o.bytes);
       comm_.bcast_many(dev_, lops, ls);
       prof_end(PH_BCAST, pb, ls);
       lops.clear();
@@ -1030,6 +1042,7 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
   if (vparts_)  // the last step's piece: no column update consumes it, the chunk pass does first
     vhash(v, vslot(V_PP, q - 1), elem(PP_[par], (q - 1) * m * (int64_t)d_ * m), (int64_t)d_ * m * (int64_t)es,
           (int64_t)d_ * m * (int64_t)es, m, S_COMM);
+  if (vlocal_on()) vlocal_hash(v, V_LC, false, S_COMM);  // Lrow / Ht / PP as the chunk pass reads them
   if (split_ == 1) deferred_updates(v, S_COMM);
   cur_phase_ = "pivot-row broadcast";
   for (int64_t i = 0; i < C; ++i) {
@@ -1078,6 +1091,7 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
     auto flush = [&]() {
       if (bops.empty()) return;
       const int pb = prof_begin(S_COMM);
+      for (const auto& o : bops) count_comm(SolveStats::CK_ROWS, (double)o.bytes);
       comm_.bcast_many(dev_, bops, S_COMM);
       prof_end(PH_BCAST, pb, S_COMM);
       bops.clear();
@@ -1126,10 +1140,12 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
       bops.push_back(BcastOp{seg, (size_t)m * W * es, (int)r.owner});
     }
     flush();
-    if (i == 0 && corrupt_step_ >= t0 && corrupt_step_ < t0 + q)  // GJ_TEST_CORRUPT (tests only)
+    if (i == 0 && corrupt_step_ >= t0 && corrupt_step_ < t0 + q &&  // GJ_TEST_CORRUPT (tests only)
+        !(corrupt_unprofiled_ && opt_.profile))
       dev_.memset2d(chunk + (corrupt_step_ - t0) * m * W * (int64_t)es, W * es, W * es, m, S_COMM);
     dev_.record(ev_b_[par][c], S_COMM);
   }
+  if (vlocal_on()) vlocal_hash(v, V_LE, false, S_COMM);  // ... and after its last read
   dev_.record(ev_cp_[par], S_COMM);
   dbg_sync();
 }
@@ -1261,6 +1277,7 @@ void Engine::big_update(int64_t u) {
     const int64_t c0 = cb0_[c] * m, c1 = cb1_[c] * m, W = c1 - c0;
     const int ms = S_MAIN;
     if (!dropped("b")) dev_.wait(ms, ev_b_[par][c]);
+    if (i == 0 && vlocal_on()) vlocal_hash(u, V_LC, true, ms);  // At as the first chunk update reads it
     if (vparts_)  // what this chunk's update is about to read, segment by segment (one root each)
       for (int64_t j = 0; j < q; ++j)
         vhash(u, vslot(V_RB, j, c), rb_chunk(par, c) + j * m * W * (int64_t)esz(), W * (int64_t)esz(),
@@ -1300,6 +1317,7 @@ void Engine::big_update(int64_t u) {
                   rb_chunk(par, c) + (ra[z] - c0) * (int64_t)esz(), W, elem(X_, ra[z]), npad, ms, ex);
       }
     prof_end(PH_UPDATE, pe, ms);
+    if (i + 1 == C && vlocal_on()) vlocal_hash(u, V_LE, true, ms);  // ... and after the last one
     dev_.record(ev_c_[c], ms);
   }
   dbg_sync();
@@ -1363,6 +1381,7 @@ SolveStats Engine::solve_steps() {
   dev_.sync_stream(S_SIDE);
 
   st.pivots.assign(Nr, -1);
+  for (int k = 0; k < SolveStats::kNumCommKinds; ++k) comm_bytes_[k] = 0, comm_calls_[k] = 0;
   live_ = L_.nblk;
   used_local_.assign((size_t)std::max<int64_t>(L_.nblk, 1), 0);
   for (int i = 0; i < 2; ++i) chain_sel_[i] = defer_sel_[i] = GemmExtra{};
@@ -1406,6 +1425,7 @@ SolveStats Engine::solve_steps() {
   const double t_end = now_s();
   for (int64_t t = 0; t < Nr; ++t)
     if (st.pivots[t] != t) st.offdiag_pivots++;
+  for (int k = 0; k < SolveStats::kNumCommKinds; ++k) st.comm_bytes[k] = comm_bytes_[k], st.comm_calls[k] = comm_calls_[k];
   if (vparts_) verify_hashes(st);  // outside the timed interval; throws VerifyFailed on every rank
   st.host_wait_ms = host_wait * 1e3;
   st.seconds = t_end - t_begin;
@@ -1417,12 +1437,48 @@ SolveStats Engine::solve_steps() {
 // ---------------------------------------------------------------- GJ_VERIFY
 int Engine::vslot(VKind k, int64_t j, int64_t c) const {
   const int64_t C = (int64_t)cb0_.size();
+  const int64_t L0 = C * d_ + 3 * d_ + 1;  // first rank-local slot
   switch (k) {
     case V_RB: return (int)(c * d_ + j);
     case V_PP: return (int)(C * d_ + j);
     case V_LA: return (int)(C * d_ + d_ + j);
     case V_RECS: return (int)(C * d_ + 2 * d_ + j);
-    default: return (int)(C * d_ + 3 * d_);
+    case V_SEQ: return (int)(C * d_ + 3 * d_);
+    case V_LP: return (int)(L0 + j);
+    case V_LC: return (int)(L0 + vlocal_groups() + j);
+    default: return (int)(L0 + 2 * vlocal_groups() + j);
+  }
+}
+
+// The bytes of rank-local hand-over group g of panel v (see VKind): empty where nothing is handed
+// over (no local rows, Lrow of a panel's first step, steps past the panel's end).
+Engine::VRegion Engine::vlocal_region(int64_t v, int g) const {
+  const int par = (int)(v & 1);
+  const int64_t m = L_.m, q = panel_q(v), es = (int64_t)esz(), dm = (int64_t)d_ * m;
+  VRegion r;
+  const std::string P = "[" + std::to_string(par) + "]";
+  if (g == 0) {
+    r.name = "multiplier panel At[" + std::to_string(v % 3) + "]";
+    if (L_.rows > 0) r = {At_[v % 3], L_.rows * es, L_.rows * es, q * m, r.name};
+  } else if (g == 1) {
+    r = {PP_[par], dm * es, q * m * es, q * m, "panel pieces PP" + P};
+  } else if (g < 2 + d_) {
+    const int64_t j = g - 2;
+    r.name = "Lrow" + P + "[" + std::to_string(j) + "]";
+    if (j >= 1 && j < q) r = {Lrow_[par][j], m * es, m * es, j * m, r.name};
+  } else {
+    const int64_t j = g - 2 - d_;
+    r.name = "Ht" + P + "[" + std::to_string(j) + "]";
+    if (j < q) r = {Ht_[par][j], m * es, m * es, m, r.name};
+  }
+  return r;
+}
+
+void Engine::vlocal_hash(int64_t v, VKind point, bool at_group, int s) {
+  for (int g = 0; g < vlocal_groups(); ++g) {
+    if ((g == 0) != at_group && point != V_LP) continue;
+    const VRegion r = vlocal_region(v, g);
+    if (r.base && r.rows > 0) vhash(v, vslot(point, g), r.base, r.ld, r.width, r.rows, s);
   }
 }
 
@@ -1466,6 +1522,16 @@ void Engine::verify_hashes(const SolveStats& st) {
       order.push_back({vslot(V_LA, j), t0 + j, "look-ahead update",
                        "look-ahead rows LA[" + std::to_string(v & 1) + "] step " + std::to_string(j), owner(t0 + j),
                        "SIDE"});
+    // rank-local hand-overs: -2 - g = compare with this rank's own producer hash of group g
+    if (vlocal_on()) {
+      for (int pt = 0; pt < 2; ++pt)
+        for (int g = 1; g < vlocal_groups(); ++g)
+          order.push_back({vslot(pt == 0 ? V_LC : V_LE, g), t0 + q - 1,
+                           pt == 0 ? "chunk pass (before its first read)" : "chunk pass (after its last read)",
+                           vlocal_region(v, g).name, -2 - g, "COMM"});
+      order.push_back({vslot(V_LC, 0), t0 + q - 1, "trailing update (before its first read)",
+                       vlocal_region(v, 0).name, -2, "MAIN"});
+    }
     for (int64_t i = 0; i < C; ++i) {
       const int64_t c = (start + i) % C;
       for (int64_t j = 0; j < q; ++j)
@@ -1474,10 +1540,30 @@ void Engine::verify_hashes(const SolveStats& st) {
                              std::to_string(j),
                          owner(t0 + j), "MAIN"});
     }
+    if (vlocal_on())
+      order.push_back({vslot(V_LE, 0), t0 + q - 1, "trailing update (after its last read)",
+                       vlocal_region(v, 0).name, -2, "MAIN"});
     for (const Item& it : order) {
+      std::vector<int64_t> bad;
+      if (it.root <= -2) {  // rank-local: each rank against what its own SIDE stream produced
+        const int g = (int)(-2 - it.root);
+        for (int64_t r = 0; r < p; ++r)
+          if (h(r, v, it.slot) != h(r, v, vslot(V_LP, g))) bad.push_back(r);
+        if (bad.empty()) continue;
+        std::string who;
+        for (int64_t r : bad) who += (who.empty() ? "" : ", ") + std::to_string(r);
+        throw Error(Status::VerifyFailed,
+                    "GJ_VERIFY: step " + std::to_string(it.step) + " (panel " + std::to_string(v) + "), phase " +
+                        it.phase + ", rank-local buffer " + it.buffer + ": rank(s) [" + who +
+                        "] saw different bytes on stream " + it.stream +
+                        " than the SIDE stream left at the end of the panel (" +
+                        (std::string(it.phase).find("before") != std::string::npos
+                             ? "read before it was written or before the write was visible"
+                             : "rewritten while still being read") +
+                        "; first mismatch in step order)");
+      }
       // reference value: the root's hash (broadcast buffers), else rank 0's (gathered / agreed state)
       const int64_t ref = it.root >= 0 ? it.root : 0;
-      std::vector<int64_t> bad;
       for (int64_t r = 0; r < p; ++r)
         if (h(r, v, it.slot) != h(ref, v, it.slot)) bad.push_back(r);
       if (bad.empty()) continue;

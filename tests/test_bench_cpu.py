@@ -112,6 +112,14 @@ def test_bench_self_launch_matches_torchrun():
     assert da["residual_inf"] < 1e-8 and abs(da["residual_inf"] - db["residual_inf"]) < 1e-12
     assert len(da["rank_solve_seconds_max"]) == 8
     assert da["policy"]["depth"] == da["config"]["depth"]
+    # achieved bandwidth per collective kind and rank, from the untimed profiled solve
+    bw = da["comm_bandwidth"]["per_rank"]
+    assert len(bw) == 8
+    for r in bw:
+        assert set(r) == {"pivot_rows", "panel_pieces", "pivot_records"}
+        assert r["pivot_rows"]["bytes"] > 0 and r["pivot_records"]["calls"] > 0
+        assert r["pivot_rows"]["GB_s"] is None or r["pivot_rows"]["GB_s"] > 0
+    assert len(da["step_ms"]) == 2
 
 
 def test_bench_self_launch_failure_exit_code():
@@ -162,6 +170,19 @@ def test_bench_wrong_inverse_fails():
     assert d["check"] == "residual_failed" and not d["residual_inf"] < d["residual_bound"]
     assert "rank exit codes [2, 2, 2, 2]" in bad.stderr
     assert "wrong inverse" in bad.stderr
+
+
+def test_bench_gate_checks_a_timed_solve():
+    """At p > 1 the bench runs one extra untimed solve with the phase timers after the timed loop
+    (another schedule).  The residual gate must check a TIMED solve: here only the unprofiled
+    solves are corrupted (GJ_TEST_CORRUPT=<rank>:<step>:unprofiled), the profiled one is clean,
+    and the run must still fail."""
+    args = ("--steps", "1", "--warmup", "0", "--size", "200", "--block", "8")
+    bad = _self_launch(2, *args, env_extra={"GJ_TEST_CORRUPT": "1:5:unprofiled"})
+    assert bad.returncode == 2, bad.stderr[-3000:]
+    d = _json_line(bad.stdout)
+    assert d["check"] == "residual_failed"
+    assert "profiled_solve" in d  # the clean profiled solve did run after the gate's solve
 
 
 def test_cli_check_residual(gj_bin):

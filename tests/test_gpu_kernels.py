@@ -319,6 +319,54 @@ def test_glds_peeled_loop_matches_reference(native, M, N, K, build):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("M,N,K", [(2948, 2900, 520), (2050, 1030, 516), (1538, 2050, 1003), (4096, 2048, 512),
+                                   (2048, 1024, 8), (1026, 514, 20), (2948, 2902, 16), (640, 200, 512)])
+@pytest.mark.parametrize("build", [33, 23, 32])
+def test_glds_tile128_matches_reference(native, M, N, K, build):
+    """The 128 x 128 LDS-DMA tile (set_glds_tile(128): 2 x 2 waves of 64 x 64, one B DMA piece per
+    k row) against the fp64 reference, with zero columns / rows, ragged edges, K not a multiple of
+    the slice; bit-identical to the 128 x 64 tile (same MFMAs in the same k order per element)."""
+    A = _rand((M, K), torch.float64, 41)
+    B = _rand((K, N), torch.float64, 42)
+    C = _rand((M, N), torch.float64, 43)
+    z0, z1, zr, zh = 128, 256, [0, 384], 128
+    Cin = C.clone()
+    Cin[:, z0:z1] = 0
+    for r in zr:
+        Cin[r:r + zh] = 0
+    ref = Cin + A @ B
+    outs = []
+    try:
+        for tile in (64, 128):
+            native.set_glds_tile(tile)
+            native.set_glds_build(build if tile == 128 else 33)
+            Cd = C.cuda()
+            ops.gemm(A.t().contiguous().cuda(), B.cuda(), Cd, op="acc", a_kmajor=True, zero_cols=(z0, z1),
+                     zero_rows=zr, zero_row_height=zh)
+            outs.append(Cd.cpu())
+    finally:
+        native.set_glds_tile(64)
+        native.set_glds_build(0)
+    assert (outs[1].double() - ref).abs().max().item() < 1e-12 * K
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_engine_tile128_bit_identical(native):
+    """The whole solve with the 128 x 128 trailing-update tile: the same inverse bits as 128 x 64."""
+    n, m = 4096, 128
+    outs = []
+    try:
+        for tile in (64, 128):
+            native.set_glds_tile(tile)
+            eng = native.Engine(native.hip_device(0), native.self_comm(), n, m, "fp64", 0, 1e-15, False, 4)
+            eng.generate("random", 3)
+            assert eng.solve()["status"] == 0
+            outs.append(eng.download_local_rows())
+    finally:
+        native.set_glds_tile(64)
+    assert np.array_equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
 @pytest.mark.parametrize("count", [1, 3, 4, 6])
 def test_gemm_batch_mixed_store_acc(dtype, count):

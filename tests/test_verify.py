@@ -70,6 +70,44 @@ def test_verify_catches_corruption_at_its_step():
                      r"root rank \d: rank\(s\) \[1\] consumed different bytes on stream MAIN", r.stderr), r.stderr
 
 
+def test_verify_names_dropped_chunk_pass_wait_on_local_buffers():
+    """GJ_TEST_DROP_WAIT=cp removes SIDE's wait for the chunk pass two panels back: SIDE then rewrites
+    a panel's multiplier rows Lrow / H_t^T / pieces (rank-local, never broadcast) while COMM's chunk
+    pass still reads them.  The rank-local hand-over hashes (producer SIDE at the panel's end, COMM
+    before its first and after its last read) name the buffer, the step and the stream -- a class the
+    broadcast hashes alone cannot see."""
+    r = _cli({"GJ_TEST_DROP_WAIT": "cp"}, "-p", "1", "--gen", "random", "--depth", "2", "--chunk-cols", "16",
+             "640", "8")
+    assert r.returncode == 2, r.stdout + r.stderr
+    assert re.search(r"GJ_VERIFY: step \d+ \(panel \d+\), phase chunk pass \(after its last read\), rank-local "
+                     r"buffer (Lrow|Ht|panel pieces PP)\[\d\](\[\d\])?: rank\(s\) \[0\] saw different bytes on "
+                     r"stream COMM than the SIDE stream left at the end of the panel \(rewritten while still being "
+                     r"read", r.stderr), r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("drop", ["edit", "x"])
+def test_verify_quiet_on_value_benign_drops(drop):
+    """The other planted drops verify cannot and must not name (profiles/verify_r6.md): 'edit' is no
+    hazard at run time (MAIN's wait for the owner edits is implied by its wait for each chunk's
+    broadcast, tests/test_race_check.py), and under 'x' the chunk pass reads the next panel's columns
+    of ITS OWN pivot rows, which the concurrent look-ahead update leaves unchanged (they are masked
+    as zero rows) -- a memory-model race the happens-before checker reports, with identical bytes.
+    No false alarm, correct inverse."""
+    r = _cli({"GJ_TEST_DROP_WAIT": drop}, "-p", "3", "--gen", "random", "--check-residual", "1e-9", "400", "16")
+    assert r.returncode == 0, r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("p", [1, 3])
+def test_verify_local_slots_clean_with_race_check(p):
+    """The rank-local hash launches are themselves ordered: the happens-before checker finds no race
+    with GJ_VERIFY on, and the verified run passes."""
+    eng = gj.GaussJordan(block_size=12, ranks=p, device="cpu", comm="async", depth=3, jitter_us=100.0,
+                         host_threads=1, race_check=True, extra=dict(verify=True))
+    rep = eng.run(300, gen="random", seed=3)
+    assert rep["status"] == 0, rep["message"]
+    assert rep["race_count"] == 0, "\n".join(rep["races"])
+
+
 def test_verify_flag_on_the_cli_and_clean_exit():
     r = subprocess.run([os.path.join(ROOT, "build", "gj"), "--device", "cpu", "-p", "3", "--verify", "--gen",
                         "random", "300", "12"], capture_output=True, text=True, timeout=180, cwd="/tmp")
