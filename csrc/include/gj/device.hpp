@@ -70,6 +70,9 @@ struct GemmExtra {
   // when the pivot chain has CUs of its own (a CU reservation), slower when it must share them
   // (profiles/gemm_stall_r4.md).
   bool dense = false;
+  // This launch's LDS-DMA build (stages * 10 + waves-per-SIMD bound: 23 | 25 | 33), 0 = by `dense`:
+  // the owner's chunk-pass normalisations under a CU reservation (Engine::chunk_build_)
+  int glds_build = 0;
   // Row-block selection (the pivot-chain / deferred split of a panel's column updates, Engine):
   // only the row blocks b (height rsel_m, b < 64 kRselWords) whose bit b of rsel is set take part;
   // M counts the selected rows ((set bits) * rsel_m) and the i-th block of M is the i-th set bit.

@@ -151,6 +151,7 @@ struct GemmArgs {
   const int32_t* pred;  // GemmExtra::owner_phys: skip unless *pred % pred_p == pred_k
   int64_t pred_p, pred_k;
   bool dense;           // GemmExtra::dense: the 5-workgroups-per-CU LDS-DMA build
+  int build;            // GemmExtra::glds_build: this launch's LDS-DMA build (0 = auto)
   uint64_t rsel[GemmExtra::kRselWords];  // GemmExtra::rsel / rsel_m: row-block selection
   int64_t rsel_m;
   int64_t skc0, skc1;   // GemmExtra::skip_c0 / skip_c1 (whole tiles)
@@ -985,12 +986,16 @@ void set_glds_build(int b) {
 }
 
 // GJ_GLDS_TILE=64|128 or set_glds_tile(): the LDS-DMA kernel's tile width (BN) for the launches
-// that take the 4-per-CU builds (the 5-per-CU dense build stays 128 x 64); profiles/gemm_tile128_r6.md
+// that take the 4-per-CU builds (the 5-per-CU dense build stays 128 x 64).  128 by default since
+// round 6 (profiles/gemm_tile128_r6.md): 32768 x 8192 x 512 alone 64.4 -> 66.8-67.3 TF/s, the
+// N = 32768 solve 1120.1 / 1119.9 -> 1083.7 / 1083.4 ms on one box (two repetitions, driver
+// command), the shader clock at the same ~1370 W 2236 -> 2287 MHz: half the LDS fragment reads
+// per MFMA and a third less operand traffic per flop buy clock under the power limit.
 static int g_glds_tile = -1;
 static int glds_tile() {
   if (g_glds_tile < 0) {
     const char* e = getenv("GJ_GLDS_TILE");
-    const int v = e ? std::atoi(e) : 64;
+    const int v = e ? std::atoi(e) : 128;
     if (v != 64 && v != 128) throw std::invalid_argument("GJ_GLDS_TILE: 64 | 128");
     g_glds_tile = v;
   }
@@ -1005,7 +1010,7 @@ template <int MODE>
 static void launch_glds(const GemmArgs& a0, hipStream_t s) {
   GemmArgs a = a0;
   const int forced0 = glds_build_forced();
-  const int build0 = forced0 ? forced0 : a.dense ? 25 : glds_peel() ? 33 : 23;
+  const int build0 = forced0 ? forced0 : a.build ? a.build : a.dense ? 25 : glds_peel() ? 33 : 23;
   if (glds_tile() == 128 && glds_peel() && build0 != 25) {
     // 128 x 128 tiles: 16 accumulator tiles per wave (128 VGPRs); <stages, W> 3.3 / 2.3 / 3.2
     a.tiles_m = (int)((a.M + glds::BM - 1) / glds::BM);
@@ -1040,7 +1045,7 @@ static void launch_glds(const GemmArgs& a0, hipStream_t s) {
   // the default at 4 workgroups per CU; under a CU reservation the 5-per-CU build (2 stages: 5 x 3
   // stages would exceed the LDS) stays.  Without the peel, 2.3 (3.3 was slower, above).
   const int forced = glds_build_forced();
-  const int build = forced ? forced : a.dense ? 25 : glds_peel() ? 33 : 23;
+  const int build = forced ? forced : a.build ? a.build : a.dense ? 25 : glds_peel() ? 33 : 23;
   if (glds_peel()) {
     if (build == 25)
       hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 5, 8, 1>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
@@ -1469,6 +1474,7 @@ static void fill_extra(GemmArgs& a, const GemmExtra* ex) {
   a.pred_p = ex ? ex->owner_p : 1;
   a.pred_k = ex ? ex->owner_k : 0;
   a.dense = ex ? ex->dense : false;
+  a.build = ex ? ex->glds_build : 0;
   a.rsel_m = ex ? ex->rsel_m : 0;
   a.cin = ex ? ex->c_in : nullptr;
   a.skc0 = ex ? ex->skip_c0 : 0;

@@ -259,6 +259,11 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // scripts/runs/r5_colupd.sh)
   lat_wide_ = reserved_cus_ > 0 && L_.p == 1 && L_.npad <= 8192;
   if (const char* e = std::getenv("GJ_LAT_GLDS")) lat_wide_ = std::atoi(e) != 0;
+  // GJ_CHUNK_BUILD=23|25|33: the LDS-DMA build of the chunk pass's normalisation GEMMs (COMM).
+  // Under a CU reservation MAIN fills its 224 CUs, so COMM's workgroups land on the 32 reserved
+  // ones, where their LDS (40 KiB each at 3 stages) decides whether an 11-wave, 95 KiB candidate
+  // inverse still fits beside them (profiles/side_latency_r5.md, profiles/chain_r6.md).
+  if (const char* e = std::getenv("GJ_CHUNK_BUILD")) chunk_build_ = std::atoi(e);
   split_ = 0;
   if (const char* e = std::getenv("GJ_SPLIT")) {
     const int v = std::atoi(e);
@@ -1113,6 +1118,7 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
         lat.latency = comm_small_tiles_;
         lat.skip_c0 = sk0;
         lat.skip_c1 = sk1;
+        lat.glds_build = chunk_build_;
         for (int64_t z = 0; z < nr; ++z) {
           const int64_t a = ra[z], w = rb[z] - ra[z];
           if (j == 0) {

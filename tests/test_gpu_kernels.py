@@ -345,7 +345,7 @@ def test_glds_tile128_matches_reference(native, M, N, K, build):
                      zero_rows=zr, zero_row_height=zh)
             outs.append(Cd.cpu())
     finally:
-        native.set_glds_tile(64)
+        native.set_glds_tile(128)  # the default
         native.set_glds_build(0)
     assert (outs[1].double() - ref).abs().max().item() < 1e-12 * K
     assert torch.equal(outs[0], outs[1])
@@ -363,7 +363,7 @@ def test_engine_tile128_bit_identical(native):
             assert eng.solve()["status"] == 0
             outs.append(eng.download_local_rows())
     finally:
-        native.set_glds_tile(64)
+        native.set_glds_tile(128)  # the default
     assert np.array_equal(outs[0], outs[1])
 
 
@@ -724,9 +724,16 @@ def test_latency_kernel_bit_identical(shape, op, extras, native):
     assert torch.equal(out[0][0], out[1][0])
     if extras == "tneg":
         assert torch.equal(out[0][1], out[1][1])
-    ref = (0 if op == "store" else (kw.get("c_in", C0)).double()) + At.t() @ B
-    if extras != "masks":
-        assert torch.allclose(out[1][0], ref, rtol=1e-12, atol=1e-10)
+    cin = (kw.get("c_in", C0)).double().clone()
+    if extras == "masks":  # masked entries enter as 0 (GemmExtra zc / zr), the product is still added
+        z0, z1 = kw["zero_cols"]
+        cin[:, z0:z1] = 0
+        for r in kw["zero_rows"]:
+            cin[r:r + kw["zero_row_height"]] = 0
+    ref = (0 if op == "store" else cin) + At.t() @ B
+    # fp64 reference for every case, masks included (the masked case compared the two
+    # in-house kernels only)
+    assert torch.allclose(out[1][0], ref, rtol=1e-12, atol=1e-10)
 
 
 def test_latency_batch_kernel_bit_identical(native):
