@@ -73,6 +73,8 @@ struct GemmExtra {
   // This launch's LDS-DMA build (stages * 10 + waves-per-SIMD bound: 23 | 25 | 33), 0 = by `dense`:
   // the owner's chunk-pass normalisations under a CU reservation (Engine::chunk_build_)
   int glds_build = 0;
+  // This launch's LDS-DMA tile width (64 | 128), 0 = the device's hint (Device::set_gemm_tile_hint)
+  int glds_tile = 0;
   // Row-block selection (the pivot-chain / deferred split of a panel's column updates, Engine):
   // only the row blocks b (height rsel_m, b < 64 kRselWords) whose bit b of rsel is set take part;
   // M counts the selected rows ((set bits) * rsel_m) and the i-th block of M is the i-th set bit.
@@ -251,6 +253,9 @@ class Device {
   // co-resident form, which the engine picks where its pivot chain waits for whole CUs).  Devices
   // with a single implementation ignore it.
   virtual void set_block_inverse_hint(int variant) { (void)variant; }
+  // Tile width of the fp64 LDS-DMA trailing-update kernel for launches that do not name one
+  // (GemmExtra::glds_tile): 128 by default, 64 where CUs are reserved for the pivot chain (Engine)
+  virtual void set_gemm_tile_hint(int bn) { (void)bn; }
   // Device scratch the candidate-inverse kernel family `variant` needs for layout L (bytes), and
   // its allocation ahead of the first block_inverse call.
   virtual size_t block_inverse_scratch_bytes(DType dt, const Layout& L, int variant) const {

@@ -214,6 +214,7 @@ class Engine {
     // every GJ_* variable set in this process's environment when the engine was built ("NAME=value"):
     // a stray schedule override is visible in every record
     std::vector<std::string> env_overrides;
+    int gemm_tile = 128;          // fp64 LDS-DMA trailing-update tile width (64 | 128)
     int split = 0;                // chain / deferred split of the column updates (split_: 0, 1, 2)
     bool lat_wide = false;        // chain column updates on the LDS-DMA kernel (lat_wide_)
     bool skip_cols = false;       // one MAIN launch per chunk around the look-ahead columns (skip_cols_)
@@ -343,7 +344,8 @@ class Engine {
   // the chain's latency GEMMs on the register-fed small fp64 kernel (GemmExtra::lat_reg): on under
   // a CU reservation (GJ_LAT_REG=0/1 overrides)
   bool lat_reg_ = false;
-  int chunk_build_ = 0;  // LDS-DMA build of the chunk pass's GEMMs (GemmExtra::glds_build; 0 = auto)
+  int chunk_build_ = 0;
+  int gemm_tile_ = 128;  // LDS-DMA tile width of this engine's launches (Device::set_gemm_tile_hint)  // LDS-DMA build of the chunk pass's GEMMs (GemmExtra::glds_build; 0 = auto)
   std::vector<char> used_local_;       // local blocks used as pivot rows so far (host copy)
   double comm_bytes_[SolveStats::kNumCommKinds] = {};  // per solve, -> SolveStats::comm_bytes
   int64_t comm_calls_[SolveStats::kNumCommKinds] = {};

@@ -63,6 +63,7 @@ class HipDevice : public Device {
                             int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
                             const PivotSelectArgs& sel, int s) override;
   void set_block_inverse_hint(int variant) override { bi_hint_ = variant; }
+  void set_gemm_tile_hint(int bn) override { tile_hint_ = bn; }
   size_t block_inverse_scratch_bytes(DType dt, const Layout& L, int variant) const override;
   void prepare_block_inverse(DType dt, const Layout& L, int variant) override;
   void candidate_maxabs(DType dt, const void* Lt, int64_t ldl, double* scores, int32_t* valid,
@@ -110,6 +111,7 @@ class HipDevice : public Device {
   int dev_ = 0;
   void* streams_[kNumStreams] = {};
   int bi_hint_ = -1;  // set_block_inverse_hint
+  int tile_hint_ = 0;  // set_gemm_tile_hint
   std::vector<void*> events_;
   void* scratch_[2] = {nullptr, nullptr};
   size_t scratch_sz_[2] = {0, 0};

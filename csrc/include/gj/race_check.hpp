@@ -200,6 +200,7 @@ class RaceCheckDevice : public Device {
                             int32_t* valid, const int32_t* used, const Layout& L, double thresh, int64_t nlive,
                             const PivotSelectArgs& sel, int s) override;
   void set_block_inverse_hint(int variant) override { inner_->set_block_inverse_hint(variant); }
+  void set_gemm_tile_hint(int bn) override { inner_->set_gemm_tile_hint(bn); }
   size_t block_inverse_scratch_bytes(DType dt, const Layout& L, int variant) const override {
     return inner_->block_inverse_scratch_bytes(dt, L, variant);
   }

@@ -152,6 +152,7 @@ struct GemmArgs {
   int64_t pred_p, pred_k;
   bool dense;           // GemmExtra::dense: the 5-workgroups-per-CU LDS-DMA build
   int build;            // GemmExtra::glds_build: this launch's LDS-DMA build (0 = auto)
+  int tile;             // GemmExtra::glds_tile: this launch's LDS-DMA tile width (0 = auto)
   uint64_t rsel[GemmExtra::kRselWords];  // GemmExtra::rsel / rsel_m: row-block selection
   int64_t rsel_m;
   int64_t skc0, skc1;   // GemmExtra::skip_c0 / skip_c1 (whole tiles)
@@ -991,39 +992,56 @@ void set_glds_build(int b) {
 // N = 32768 solve 1120.1 / 1119.9 -> 1083.7 / 1083.4 ms on one box (two repetitions, driver
 // command), the shader clock at the same ~1370 W 2236 -> 2287 MHz: half the LDS fragment reads
 // per MFMA and a third less operand traffic per flop buy clock under the power limit.
-static int g_glds_tile = -1;
-static int glds_tile() {
+// Forced for every launch by GJ_GLDS_TILE / set_glds_tile(64 | 128); otherwise per launch
+// (GemmArgs::tile from GemmExtra::glds_tile or the device hint), 128 when unnamed.  Under a CU
+// reservation the engine names 64: N = 8192 22.68 / 22.69 ms (64) vs 23.52 / 23.53 (128), N = 16384
+// even (scripts/runs/r6_small128.sh).
+static int g_glds_tile = -1;  // -1 unread, 0 per launch, 64 / 128 forced
+static int glds_tile(const GemmArgs& a) {
   if (g_glds_tile < 0) {
     const char* e = getenv("GJ_GLDS_TILE");
-    const int v = e ? std::atoi(e) : 128;
-    if (v != 64 && v != 128) throw std::invalid_argument("GJ_GLDS_TILE: 64 | 128");
+    const int v = e ? std::atoi(e) : 0;
+    if (v != 0 && v != 64 && v != 128) throw std::invalid_argument("GJ_GLDS_TILE: 64 | 128");
     g_glds_tile = v;
   }
-  return g_glds_tile;
+  return g_glds_tile ? g_glds_tile : a.tile == 64 ? 64 : 128;
 }
 void set_glds_tile(int bn) {
-  if (bn != 64 && bn != 128) throw std::invalid_argument("glds tile: 64 | 128");
+  if (bn != 0 && bn != 64 && bn != 128) throw std::invalid_argument("glds tile: 0 (per launch) | 64 | 128");
   g_glds_tile = bn;
+}
+
+// GJ_GLDS_GROUP=<G>: tile rows walked together per XCD (A/B runs; default 4)
+static int glds_group() {
+  static const int g = [] {
+    const char* e = getenv("GJ_GLDS_GROUP");
+    const int v = e ? std::atoi(e) : 4;
+    return v > 0 ? v : 4;
+  }();
+  return g;
 }
 
 template <int MODE>
 static void launch_glds(const GemmArgs& a0, hipStream_t s) {
   GemmArgs a = a0;
   const int forced0 = glds_build_forced();
-  const int build0 = forced0 ? forced0 : a.build ? a.build : a.dense ? 25 : glds_peel() ? 33 : 23;
-  if (glds_tile() == 128 && glds_peel() && build0 != 25) {
-    // 128 x 128 tiles: 16 accumulator tiles per wave (128 VGPRs); <stages, W> 3.3 / 2.3 / 3.2
+  const int build0 = forced0 ? forced0 : a.build ? a.build : a.dense ? 25 : 23;
+  if (glds_tile(a) == 128 && glds_peel() && build0 != 25) {
+    // 128 x 128 tiles: 16 accumulator tiles per wave (128 VGPRs); <stages, W> 2.3 (auto) / 3.3 / 3.2.
+    // Two stages by default: as fast alone as three (66.80 / 67.23 vs 66.83 / 67.25 TF/s), and 3 x
+    // 34 KiB instead of 3 x 51 KiB per CU leaves 56 KiB of LDS free, so a co-resident candidate
+    // inverse (72 KiB) starts when ONE trailing-update workgroup retires (profiles/gemm_tile128_r6.md)
     a.tiles_m = (int)((a.M + glds::BM - 1) / glds::BM);
     a.tiles_n = (int)((a.N + 127) / 128);
     const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;
     if (nwg <= 0) return;
-    a.group = 4;
-    if (build0 == 23)
-      hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 3, 8, 1, 128>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
+    a.group = glds_group();
+    if (build0 == 33)
+      hipLaunchKernelGGL((gemm_glds_f64<MODE, 3, 3, 8, 1, 128>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
     else if (build0 == 32)
       hipLaunchKernelGGL((gemm_glds_f64<MODE, 3, 2, 8, 1, 128>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
     else
-      hipLaunchKernelGGL((gemm_glds_f64<MODE, 3, 3, 8, 1, 128>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
+      hipLaunchKernelGGL((gemm_glds_f64<MODE, 2, 3, 8, 1, 128>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
     return;
   }
   a.tiles_m = (int)((a.M + glds::BM - 1) / glds::BM);
@@ -1475,6 +1493,7 @@ static void fill_extra(GemmArgs& a, const GemmExtra* ex) {
   a.pred_k = ex ? ex->owner_k : 0;
   a.dense = ex ? ex->dense : false;
   a.build = ex ? ex->glds_build : 0;
+  a.tile = ex ? ex->glds_tile : 0;
   a.rsel_m = ex ? ex->rsel_m : 0;
   a.cin = ex ? ex->c_in : nullptr;
   a.skc0 = ex ? ex->skip_c0 : 0;

@@ -25,7 +25,7 @@ void set_glds_covl(int on);   // fp64 LDS-DMA kernel: C loads overlapped with th
 void set_lat_glds(int on);   // every latency GEMM of >= 1024 rows on the LDS-DMA kernel (tests; GemmExtra::lat_wide per call)
 void set_lat_kernel(int mode); // fp64 latency GEMMs on the register-fed kernel: 1 / 0 forced, -1 per launch (GemmExtra::lat_reg)
 void set_glds_build(int b);  // 23 | 25 | 33 (stages * 10 + waves-per-SIMD bound), 0 = auto
-void set_glds_tile(int bn);  // 64 | 128: the fp64 LDS-DMA kernel's tile width (GJ_GLDS_TILE)
+void set_glds_tile(int bn);  // 64 | 128: the fp64 LDS-DMA kernel's tile width for every launch, 0 = per launch (GJ_GLDS_TILE)
 void set_block_inverse_variant(int v);  // 0 = default families, 1 = register sweep, 5 = co-resident, 6 = generic
 int block_inverse_variant();
 int block_inverse_variant_id(const char* name);  // panel | sweep | co | generic; else throws

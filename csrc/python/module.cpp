@@ -192,7 +192,8 @@ PYBIND11_MODULE(_C, mod) {
   mod.def("set_glds_build", [](int b) { kern::set_glds_build(b); },
           "fp64 LDS-DMA trailing-update build for every launch: 23 | 25 | 33 | 43 | 1623, 0 = auto (GJ_GLDS_BUILD)");
   mod.def("set_glds_tile", [](int bn) { kern::set_glds_tile(bn); },
-          "fp64 LDS-DMA trailing-update tile width for the 4-per-CU builds: 64 | 128 (GJ_GLDS_TILE)");
+          "fp64 LDS-DMA trailing-update tile width for the 4-per-CU builds: 64 | 128 for every launch, 0 = per "
+          "launch (the engine's choice; GJ_GLDS_TILE)");
   mod.def("set_lat_kernel", [](int mode) { kern::set_lat_kernel(mode); },
           "fp64 latency GEMMs on the register-fed small kernel: 1 / 0 for every launch, -1 per launch "
           "(GemmExtra::lat_reg; GJ_LAT_KERNEL)");
@@ -503,6 +504,7 @@ PYBIND11_MODULE(_C, mod) {
                                d["pivot"] = pl.pivot;
                                if (!pl.fault_injection.empty()) d["fault_injection"] = pl.fault_injection;
                                d["env_overrides"] = pl.env_overrides;
+                               d["gemm_tile"] = pl.gemm_tile;
                                d["split"] = pl.split;
                                d["lat_wide"] = pl.lat_wide;
                                d["skip_cols"] = pl.skip_cols;

@@ -349,8 +349,15 @@ void HipDevice::h_block(DType dt, void* R, int64_t ldr, const void* Ht, int64_t 
 void HipDevice::gemm(DType dt, GemmOp op, ALayout al, int64_t M, int64_t N, int64_t K, const void* A,
                      int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int s,
                      const GemmExtra& ex) {
+  const GemmExtra* e = &ex;
+  GemmExtra hinted;
+  if (!ex.glds_tile && tile_hint_) {
+    hinted = ex;
+    hinted.glds_tile = tile_hint_;
+    e = &hinted;
+  }
   kern::gemm(dt, op == GemmOp::Acc ? 0 : 1, al == ALayout::KMajor ? 1 : 0, M, N, K, A, lda, B, ldb,
-             C, ldc, hs(streams_[s]), &ex);
+             C, ldc, hs(streams_[s]), e);
   check_launch();
 }
 void HipDevice::gemm_batch(DType dt, const GemmDesc* d, int n, int s) {

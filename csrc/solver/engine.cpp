@@ -145,6 +145,11 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // the reservation, 25.06 vs 25.43 ms; N = 16384 keeps 5 per CU, 153.9 vs 156.1 ms,
   // profiles/gemm_peel_r5.md)
   dense_gemm_ = reserved_cus_ > 0 && !(L_.p == 1 && L_.npad <= 8192);
+  // The 128 x 128 trailing-update tile (3 per CU) where the GEMM is the critical path; the 128 x 64
+  // tile (4 per CU) where CUs are reserved for the chain (N = 8192: 22.7 vs 23.5 ms,
+  // profiles/gemm_tile128_r6.md)
+  gemm_tile_ = reserved_cus_ > 0 ? 64 : 128;
+  dev_.set_gemm_tile_hint(gemm_tile_);
   if (const char* e = std::getenv("GJ_DENSE_GEMM")) dense_gemm_ = std::atoi(e) != 0;
   // Candidate inverses on ranks whose trailing update holds every CU (p > 1 without a reservation:
   // the 16384- and 8192-row ranks of N = 32768) take the co-resident 4-wave form, which starts in
@@ -283,6 +288,7 @@ Engine::Policy Engine::policy() const {
   Policy p;
   p.depth = d_;
   p.env_overrides = env_overrides_;
+  p.gemm_tile = gemm_tile_;
   p.nchunks = (int)cb0_.size();
   for (size_t c = 0; c < cb0_.size(); ++c) p.chunk_cols = std::max(p.chunk_cols, chunk_w((int64_t)c));
   p.reserve_cus = reserved_cus_;
@@ -1359,6 +1365,7 @@ SolveStats Engine::solve_steps() {
 
   comm_.barrier(dev_);
   const double t_begin = now_s();
+  dev_.set_gemm_tile_hint(gemm_tile_);  // (the device may be shared with another engine)
 
   norm_a_ = norm_inf();
   local_norm_valid_ = false;  // the sweep consumes X

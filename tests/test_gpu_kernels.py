@@ -345,7 +345,7 @@ def test_glds_tile128_matches_reference(native, M, N, K, build):
                      zero_rows=zr, zero_row_height=zh)
             outs.append(Cd.cpu())
     finally:
-        native.set_glds_tile(128)  # the default
+        native.set_glds_tile(0)  # per launch (the default)
         native.set_glds_build(0)
     assert (outs[1].double() - ref).abs().max().item() < 1e-12 * K
     assert torch.equal(outs[0], outs[1])
@@ -363,7 +363,7 @@ def test_engine_tile128_bit_identical(native):
             assert eng.solve()["status"] == 0
             outs.append(eng.download_local_rows())
     finally:
-        native.set_glds_tile(128)  # the default
+        native.set_glds_tile(0)  # per launch (the default)
     assert np.array_equal(outs[0], outs[1])
 
 
