@@ -34,6 +34,11 @@ void ShadowComm::group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) {
   size_t busiest = 0;
   for (int q = 0; q < p_; ++q) busiest = std::max({busiest, out[q], in[q]});
   cost(dev, busiest, 1, s);
+  // what the synthetic peers send arrives as zeros, as in bcast(): the direct broadcast's slices
+  // used to keep whatever the buffer held (uninitialised on first use -- an intermittent
+  // "singular matrix" of the emulated rank, tests/test_shadow_model.py)
+  for (const auto& o : ops)
+    if (!o.send) dev.memset0(o.ptr, o.bytes, s);
 }
 
 ShadowComm::~ShadowComm() {

@@ -145,10 +145,12 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // the reservation, 25.06 vs 25.43 ms; N = 16384 keeps 5 per CU, 153.9 vs 156.1 ms,
   // profiles/gemm_peel_r5.md)
   dense_gemm_ = reserved_cus_ > 0 && !(L_.p == 1 && L_.npad <= 8192);
-  // The 128 x 128 trailing-update tile (3 per CU) where the GEMM is the critical path; the 128 x 64
-  // tile (4 per CU) where CUs are reserved for the chain (N = 8192: 22.7 vs 23.5 ms,
-  // profiles/gemm_tile128_r6.md)
-  gemm_tile_ = reserved_cus_ > 0 ? 64 : 128;
+  // The 128 x 128 trailing-update tile (3 per CU) on ranks of more than 8192 rows without a CU
+  // reservation, where the GEMM is the critical path (N = 32768: 1120 -> 1083.5 ms on one box;
+  // emulated p = 2: even); the 128 x 64 tile (4 per CU) elsewhere: under a reservation (N = 8192:
+  // 22.7 vs 23.5 ms) and on the 8192-row ranks of p = 4 at N = 32768 (emulated 0.2735 vs 0.2911 s
+  // comm-free), whose pivot chain needs the slots (profiles/gemm_tile128_r6.md)
+  gemm_tile_ = (reserved_cus_ == 0 && L_.max_nblk * L_.m > 8192) ? 128 : 64;
   dev_.set_gemm_tile_hint(gemm_tile_);
   if (const char* e = std::getenv("GJ_DENSE_GEMM")) dense_gemm_ = std::atoi(e) != 0;
   // Candidate inverses on ranks whose trailing update holds every CU (p > 1 without a reservation:
