@@ -344,8 +344,9 @@ class Engine {
   // the chain's latency GEMMs on the register-fed small fp64 kernel (GemmExtra::lat_reg): on under
   // a CU reservation (GJ_LAT_REG=0/1 overrides)
   bool lat_reg_ = false;
-  int chunk_build_ = 0;
-  int gemm_tile_ = 128;  // LDS-DMA tile width of this engine's launches (Device::set_gemm_tile_hint)  // LDS-DMA build of the chunk pass's GEMMs (GemmExtra::glds_build; 0 = auto)
+  int chunk_build_ = 0;  // LDS-DMA build of the chunk pass's GEMMs (GemmExtra::glds_build; 0 = auto)
+  int chunk_tile_ = 0;   // ... and their tile width (GemmExtra::glds_tile; 0 = gemm_tile_; A/B runs)
+  int gemm_tile_ = 128;  // LDS-DMA tile width of this engine's launches (Device::set_gemm_tile_hint)
   std::vector<char> used_local_;       // local blocks used as pivot rows so far (host copy)
   double comm_bytes_[SolveStats::kNumCommKinds] = {};  // per solve, -> SolveStats::comm_bytes
   int64_t comm_calls_[SolveStats::kNumCommKinds] = {};

@@ -271,6 +271,7 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // ones, where their LDS (40 KiB each at 3 stages) decides whether an 11-wave, 95 KiB candidate
   // inverse still fits beside them (profiles/side_latency_r5.md, profiles/chain_r6.md).
   if (const char* e = std::getenv("GJ_CHUNK_BUILD")) chunk_build_ = std::atoi(e);
+  if (const char* e = std::getenv("GJ_CHUNK_TILE")) chunk_tile_ = std::atoi(e);  // 64 | 128 (A/B)
   split_ = 0;
   if (const char* e = std::getenv("GJ_SPLIT")) {
     const int v = std::atoi(e);
@@ -1127,6 +1128,7 @@ void Engine::chunk_pipeline(int64_t v, bool wait_main) {
         lat.skip_c0 = sk0;
         lat.skip_c1 = sk1;
         lat.glds_build = chunk_build_;
+        lat.glds_tile = chunk_tile_;
         for (int64_t z = 0; z < nr; ++z) {
           const int64_t a = ra[z], w = rb[z] - ra[z];
           if (j == 0) {
