@@ -201,6 +201,7 @@ class ShadowComm : public Comm {
   std::string describe() const override;
   void allgather(Device& dev, const void* send, void* recv, size_t bytes, int s) override;
   void bcast(Device& dev, void* buf, size_t bytes, int root, int s) override;
+  void bcast_many(Device& dev, const std::vector<BcastOp>& ops, int s) override;
   void allreduce_max(Device&, double*, size_t, int) override {}
   // ring all-reduce cost (2 (p-1)/p of the bytes over one link); the synthetic peers add zeros
   void allreduce_sum(Device& dev, void* buf, size_t count, DType dt, int s) override;

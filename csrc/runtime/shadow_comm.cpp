@@ -34,11 +34,15 @@ void ShadowComm::group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) {
   size_t busiest = 0;
   for (int q = 0; q < p_; ++q) busiest = std::max({busiest, out[q], in[q]});
   cost(dev, busiest, 1, s);
-  // what the synthetic peers send arrives as zeros, as in bcast(): the direct broadcast's slices
-  // used to keep whatever the buffer held (uninitialised on first use -- an intermittent
-  // "singular matrix" of the emulated rank, tests/test_shadow_model.py)
+}
+
+// What the synthetic peers broadcast arrives as zeros, one memset per message as in the ring path
+// (bcast): the direct path's receives used to keep whatever the buffer held -- uninitialised on
+// first use, an intermittent "singular matrix" of the emulated rank (tests/test_shadow_model.py).
+void ShadowComm::bcast_many(Device& dev, const std::vector<BcastOp>& ops, int s) {
+  Comm::bcast_many(dev, ops, s);
   for (const auto& o : ops)
-    if (!o.send) dev.memset0(o.ptr, o.bytes, s);
+    if (use_direct(o.bytes) && o.root != 0) dev.memset0(o.buf, o.bytes, s);
 }
 
 ShadowComm::~ShadowComm() {
@@ -95,7 +99,7 @@ void ShadowComm::allreduce_sum(Device& dev, void*, size_t count, DType dt, int s
 }
 
 void ShadowComm::bcast(Device& dev, void* buf, size_t bytes, int root, int s) {
-  if (use_direct(bytes)) return bcast_direct(dev, {BcastOp{buf, bytes, root}}, s);
+  if (use_direct(bytes)) return bcast_many(dev, {BcastOp{buf, bytes, root}}, s);
   cost(dev, bytes, 1, s);
   if (root != 0) dev.memset0(buf, bytes, s);
 }
