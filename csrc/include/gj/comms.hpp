@@ -219,6 +219,7 @@ class ShadowComm : public Comm {
 
  private:
   void cost(Device& dev, size_t bytes, int links, int s);
+  void receive_zeros(Device& dev, void* buf, size_t bytes, int s);
   int p_;
   CostModel cm_;
   int64_t step_ = 0;

@@ -185,6 +185,13 @@ class Device {
   virtual void occupy(int s, int nwg, double us, int lds_bytes = 0) {
     (void)s; (void)nwg; (void)us; (void)lds_bytes;
   }
+  // Zero `bytes` at p on stream s with `nwg` workgroups of an RCCL channel's footprint (the data a
+  // synthetic peer "sends" in ShadowComm's cost model, written with the CU footprint of the
+  // receiving channel kernels rather than a full-chip fill kernel).  Default: memset0.
+  virtual void zero_channels(void* p, size_t bytes, int s, int nwg, int lds_bytes) {
+    (void)nwg; (void)lds_bytes;
+    memset0(p, bytes, s);
+  }
   // Keep the MAIN (trailing-update) stream off `n` CUs so the latency-critical SIDE/COMM kernels
   // always find idle CUs (the first n bits of the CU mask; n = 32 is one CU per shader engine).
   // Returns the number of CUs actually reserved.  Call while the device is idle.

@@ -47,6 +47,7 @@ class HipDevice : public Device {
   std::shared_ptr<void> mark(int s) override;
   void wait_mark(int s, const std::shared_ptr<void>& h) override;
   void occupy(int s, int nwg, double us, int lds_bytes = 0) override;
+  void zero_channels(void* p, size_t bytes, int s, int nwg, int lds_bytes) override;
 
   void generate(DType dt, void* X, const Layout& L, GenSpec g, int s) override;
   void widen(DType dt, double* dst, int64_t ldd, const void* X, int64_t ldx, int64_t rows, int64_t cols,

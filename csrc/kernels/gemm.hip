@@ -1116,16 +1116,22 @@ __device__ __forceinline__ void wait_slices(int n) {  // the pieces of the n new
 }
 
 // PEEL = 1: the fp64 kernel's peeled, stage-unrolled steady state (gemm_glds_f64), for fp32.
-template <int MODE, int NS, int OCC, int BK, int PEEL = 0>
+// BNT = 256 (round 6, as the fp64 128 x 128 tile): 2 x 2 waves of 64 x 128, 128 accumulator VGPRs,
+// a third fewer LDS fragment reads per MFMA and a quarter less staged operand traffic per flop; a B
+// k row is then 1 KiB, one DMA piece (profiles/gemm_tile128_r6.md, fp32 section).
+template <int MODE, int NS, int OCC, int BK, int PEEL = 0, int BNT = glds32::BN>
 __global__ __launch_bounds__(glds32::NT, OCC) void gemm_glds_f32(GemmArgs g) {
   using namespace glds32;
   if (gemm_skipped(g)) return;
   static_assert(NS >= 2 && NS <= 4, "stages");
   static_assert(BK == 8 || BK == 16 || BK == 32, "slice depth");
+  static_assert(BNT == 128 || BNT == 256, "tile width");
+  constexpr int BN = BNT;  // (shadows glds32::BN)
   constexpr int SA = BK * BM, SB = BK * BN, STAGE = SA + SB;
-  constexpr int PIECES = BK / 8 + BK / 8;  // per wave per slice: A rows, B rows (2 per piece)
+  constexpr int BPW = BN == 256 ? BK / 4 : BK / 8;  // B pieces per wave per slice (1 / 2 k rows each)
+  constexpr int PIECES = BK / 8 + BPW;  // per wave per slice: A rows (2 per piece), B rows
   typedef float acc_t __attribute__((ext_vector_type(16)));
-  constexpr int ES = 4, TM = 64, TN = 64, MI = 2, NJ = 2, WN = 2;
+  constexpr int ES = 4, TM = 64, TN = BN / 2, MI = 2, NJ = TN / 32, WN = 2;
   __shared__ float lds[NS * STAGE];
 
   const int nwg = g.tiles_m * g.tiles_n;
@@ -1200,9 +1206,13 @@ __global__ __launch_bounds__(glds32::NT, OCC) void gemm_glds_f32(GemmArgs g) {
         for (int q = 0; q < 16; ++q) asm volatile("" ::"v"(acc[i][j][q]));
   }
 
-  // DMA piece (per wave): k rows 2 (wid + 4h) + (lane >> 5), floats 4 (lane & 31) .. + 3
+  // DMA piece (per wave): k rows 2 (wid + 4h) + (lane >> 5), floats 4 (lane & 31) .. + 3; B at
+  // BN = 256: k rows wid + 4h, floats 4 lane .. + 3
   const int dcol = 4 * (lane & 31), drow = lane >> 5;
-  const bool a_ok = (m0L + dcol) < g.M, b_ok = (n0 + dcol) < g.N;
+  const int bdcol = BN == 256 ? 4 * lane : dcol;
+  const bool a_ok = (m0L + dcol) < g.M, b_ok = (n0 + bdcol) < g.N;
+  auto bkp = [&](int h) { return BN == 256 ? wid + 4 * h : 2 * (wid + 4 * h); };   // LDS k row of piece h
+  auto bkr = [&](int h) { return BN == 256 ? wid + 4 * h : 2 * (wid + 4 * h) + drow; };  // its global k row
   __amdgpu_buffer_rsrc_t ra = rsrc(A + m0);
   __amdgpu_buffer_rsrc_t rb = rsrc(B + n0);
   const int Kd = (int)g.K;
@@ -1217,11 +1227,11 @@ __global__ __launch_bounds__(glds32::NT, OCC) void gemm_glds_f32(GemmArgs g) {
                                                ok ? ((k0 + kr) * lda + dcol) * ES : kOOB, 0, 0, 0);
     }
 #pragma unroll
-    for (int h = 0; h < BK / 8; ++h) {
-      const int kp = 2 * (wid + 4 * h), kr = kp + drow;
+    for (int h = 0; h < BPW; ++h) {
+      const int kp = bkp(h), kr = bkr(h);
       const bool ok = b_ok && (k0 + kr) < Kd;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (__attribute__((address_space(3))) void*)(st + SA + kp * BN),
-                                               16, ok ? ((k0 + kr) * ldb + dcol) * ES : kOOB, 0, 0, 0);
+                                               16, ok ? ((k0 + kr) * ldb + bdcol) * ES : kOOB, 0, 0, 0);
     }
   };
   // fragments of k step kk + 2 are read while the MFMAs of step kk run (two register sets)
@@ -1265,13 +1275,14 @@ __global__ __launch_bounds__(glds32::NT, OCC) void gemm_glds_f32(GemmArgs g) {
     // steady state, NS slices per trip, every slice it issues (up to kt + 2 NS - 2) full: fixed
     // per-lane DMA offsets + the slice offset in an SGPR, compile-time stages, constant waits
     const int nfull = Kd / BK;
-    int va[BK / 8], vb[BK / 8];
+    int va[BK / 8], vb[BPW];
 #pragma unroll
     for (int h = 0; h < BK / 8; ++h) {
       const int kr = 2 * (wid + 4 * h) + drow;
       va[h] = a_ok ? (kr * lda + dcol) * ES : kOOB;
-      vb[h] = b_ok ? (kr * ldb + dcol) * ES : kOOB;
     }
+#pragma unroll
+    for (int h = 0; h < BPW; ++h) vb[h] = b_ok ? (bkr(h) * ldb + bdcol) * ES : kOOB;
     const int sa_step = __builtin_amdgcn_readfirstlane(BK * lda * ES);
     const int sb_step = __builtin_amdgcn_readfirstlane(BK * ldb * ES);
     for (; kt + 2 * NS - 2 < nfull; kt += NS) {
@@ -1282,7 +1293,7 @@ __global__ __launch_bounds__(glds32::NT, OCC) void gemm_glds_f32(GemmArgs g) {
 #pragma unroll
         for (int h = 0; h < BK / 8; ++h) dma16f(ra, st + 2 * (wid + 4 * h) * BM, va[h], kn * sa_step);
 #pragma unroll
-        for (int h = 0; h < BK / 8; ++h) dma16f(rb, st + SA + 2 * (wid + 4 * h) * BN, vb[h], kn * sb_step);
+        for (int h = 0; h < BPW; ++h) dma16f(rb, st + SA + bkp(h) * BN, vb[h], kn * sb_step);
         compute_st(S0);
         wait_vm<PIECES * (NS - 2)>();  // slice kt + S0 + 1 landed; the NS - 2 newest may fly
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1317,6 +1328,17 @@ __global__ __launch_bounds__(glds32::NT, OCC) void gemm_glds_f32(GemmArgs g) {
 template <int MODE>
 static void launch_glds32(const GemmArgs& a0, hipStream_t s) {
   GemmArgs a = a0;
+  // the wide tile where the engine (or GJ_GLDS_TILE=128) names the wide fp64 tile
+  const bool skip_ok = !(a.skc1 > a.skc0) || (a.skc0 % 256 == 0 && a.skc1 % 256 == 0);  // whole tiles
+  if (glds_tile(a) == 128 && glds_peel() && skip_ok) {
+    a.tiles_m = (int)((a.M + glds32::BM - 1) / glds32::BM);
+    a.tiles_n = (int)((a.N + 255) / 256);
+    const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;
+    if (nwg <= 0) return;
+    a.group = 4;
+    hipLaunchKernelGGL((gemm_glds_f32<MODE, 2, 3, 16, 1, 256>), dim3((unsigned)nwg), dim3(glds32::NT), 0, s, a);
+    return;
+  }
   a.tiles_m = (int)((a.M + glds32::BM - 1) / glds32::BM);
   a.tiles_n = (int)((a.N + glds32::BN - 1) / glds32::BN);
   const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;

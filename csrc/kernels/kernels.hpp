@@ -87,6 +87,9 @@ void extract_neg_t(DType dt, void* Lt, int64_t ldl, const void* X, int64_t ldx, 
 void add_diag(DType dt, void* A, int64_t ld, int64_t nd, double alpha, hipStream_t s);
 // nwg workgroups that each spin for `us` microseconds (lds_bytes > 0: 256 threads + that much LDS)
 void spin(int nwg, double us, hipStream_t s, int lds_bytes = 0);
+// zero `bytes` at p (16-byte vector stores, scalar tail) on nwg 256-thread workgroups holding
+// lds_bytes of LDS each: the receiving RCCL channels' footprint in ShadowComm's cost model
+void zero_channels(void* p, size_t bytes, int nwg, int lds_bytes, hipStream_t s);
 void pivot_local(const double* scores, const int32_t* valid, const int32_t* used, const int32_t* pos,
                  const Layout& L, PivotRec* out, hipStream_t s);
 void pivot_select_single(const double* scores, const int32_t* valid, const Layout& L, int32_t t,

@@ -207,6 +207,30 @@ void spin(int nwg, double us, hipStream_t s, int lds_bytes) {
     hipLaunchKernelGGL(spin_kernel, dim3((unsigned)nwg), dim3(64), 0, s, ticks);
 }
 
+// The receiving channels of a modelled transfer write its bytes (ShadowComm): zeros, 16-byte vector
+// stores spread over the launched workgroups, the same 140-VGPR / LDS footprint as spin_channel_kernel.
+__global__ __launch_bounds__(256) void zero_channel_kernel(uint4* p, size_t n16, unsigned char* tail, int ntail) {
+  asm volatile("v_mov_b32 v139, 0" ::: "v139");
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) p[i] = z;
+  if (blockIdx.x == 0 && (int)threadIdx.x < ntail) tail[threadIdx.x] = 0;
+}
+
+void zero_channels(void* p, size_t bytes, int nwg, int lds_bytes, hipStream_t s) {
+  if (!bytes || nwg <= 0) return;
+  // the engine's buffers are 16-byte aligned; a misaligned head goes to hipMemsetAsync
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  if (a & 15) {
+    (void)hipMemsetAsync(p, 0, bytes, s);
+    return;
+  }
+  const size_t n16 = bytes / 16;
+  const int ntail = (int)(bytes % 16);
+  hipLaunchKernelGGL(zero_channel_kernel, dim3((unsigned)nwg), dim3(256), (size_t)lds_bytes, s,
+                     static_cast<uint4*>(p), n16, static_cast<unsigned char*>(p) + n16 * 16, ntail);
+}
+
 template <typename T>
 __global__ void add_diag_kernel(T* A, int64_t ld, int64_t nd, double alpha) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -208,6 +208,11 @@ void HipDevice::occupy(int s, int nwg, double us, int lds_bytes) {
   kern::spin(nwg, us, hs(streams_[s]), lds_bytes);
   check_launch();
 }
+void HipDevice::zero_channels(void* p, size_t bytes, int s, int nwg, int lds_bytes) {
+  if (!bytes) return;
+  kern::zero_channels(p, bytes, nwg, lds_bytes, hs(streams_[s]));
+  check_launch();
+}
 
 void* HipDevice::scratch(size_t bytes, int slot) {
   if (bytes > scratch_sz_[slot]) {

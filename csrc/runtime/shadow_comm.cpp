@@ -42,7 +42,15 @@ void ShadowComm::group_p2p(Device& dev, const std::vector<P2POp>& ops, int s) {
 void ShadowComm::bcast_many(Device& dev, const std::vector<BcastOp>& ops, int s) {
   Comm::bcast_many(dev, ops, s);
   for (const auto& o : ops)
-    if (use_direct(o.bytes) && o.root != 0) dev.memset0(o.buf, o.bytes, s);
+    if (use_direct(o.bytes) && o.root != 0) receive_zeros(dev, o.buf, o.bytes, s);
+}
+
+// Under the cost model the channel workgroups that model the transfer also write its bytes (zeros,
+// 16 workgroups of the RCCL channel footprint: the receive side of a real transfer, not a full-chip
+// fill kernel on the CUs the pivot chain needs); comm-free, a plain memset.
+void ShadowComm::receive_zeros(Device& dev, void* buf, size_t bytes, int s) {
+  if (cm_.bw_gbs > 0) dev.zero_channels(buf, bytes, s, cm_.channels, cm_.lds_kib << 10);
+  else dev.memset0(buf, bytes, s);
 }
 
 ShadowComm::~ShadowComm() {
@@ -101,7 +109,7 @@ void ShadowComm::allreduce_sum(Device& dev, void*, size_t count, DType dt, int s
 void ShadowComm::bcast(Device& dev, void* buf, size_t bytes, int root, int s) {
   if (use_direct(bytes)) return bcast_many(dev, {BcastOp{buf, bytes, root}}, s);
   cost(dev, bytes, 1, s);
-  if (root != 0) dev.memset0(buf, bytes, s);
+  if (root != 0) receive_zeros(dev, buf, bytes, s);
 }
 
 void ShadowComm::host_allgather(Device&, const void* send, void* recv, size_t bytes) {

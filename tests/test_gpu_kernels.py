@@ -351,6 +351,35 @@ def test_glds_tile128_matches_reference(native, M, N, K, build):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("M,N,K", [(4096, 4096, 512), (2052, 1028, 520), (1028, 2060, 100), (640, 256, 512),
+                                   (1024, 264, 16)])
+def test_glds32_tile256_matches_reference(native, M, N, K):
+    """The fp32 LDS-DMA kernel's 128 x 256 tile (taken where the wide fp64 tile is named,
+    set_glds_tile(128): 2 x 2 waves of 64 x 128, one B DMA piece per k row) against an fp64
+    reference and bit-identical to the 128 x 128 fp32 tile; zero columns / rows, ragged edges."""
+    A = _rand((M, K), torch.float32, 51)
+    B = _rand((K, N), torch.float32, 52)
+    C = _rand((M, N), torch.float32, 53)
+    z0, z1, zr, zh = 128, 256, [0, 512], 128
+    Cin = C.double().clone()
+    Cin[:, z0:z1] = 0
+    for r in zr:
+        Cin[r:r + zh] = 0
+    ref = Cin + A.double() @ B.double()
+    outs = []
+    try:
+        for tile in (64, 128):
+            native.set_glds_tile(tile)
+            Cd = C.cuda()
+            ops.gemm(A.t().contiguous().cuda(), B.cuda(), Cd, op="acc", a_kmajor=True, zero_cols=(z0, z1),
+                     zero_rows=zr, zero_row_height=zh)
+            outs.append(Cd.cpu())
+    finally:
+        native.set_glds_tile(0)
+    assert ((outs[1].double() - ref).abs().max() / ref.abs().max()).item() < 1e-5
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_engine_tile128_bit_identical(native):
     """The whole solve with the 128 x 128 trailing-update tile: the same inverse bits as 128 x 64."""
     n, m = 4096, 128
