@@ -19,7 +19,7 @@ HIPFLAGS  := $(COMMON) --offload-arch=$(ARCH) -mcode-object-version=5 -munsafe-f
 HOSTFLAGS := $(COMMON) -x c++ -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
 LDLIBS    := -L$(ROCM)/lib -lrccl -lamdhip64 -lrocprofiler-sdk-roctx -lpthread
 
-KERNELS   := gemm blockinv blockinv_mfma blockinv_big misc
+KERNELS   := gemm blockinv blockinv_mfma blockinv_big blockinv_huge misc
 HOST_SRC  := solver/engine solver/runner runtime/host_device runtime/hip_device \
              runtime/loopback_comm runtime/async_loopback_comm runtime/async_host_device \
              runtime/shadow_comm runtime/rccl_comm runtime/comm runtime/race_check io/matrix_io

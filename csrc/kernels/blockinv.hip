@@ -754,9 +754,10 @@ static bool launch_blocked(const void* Lt, int64_t ldl, void* inv_t, double* sco
 }
 
 // 0 = matrix-core panels (default: blockinv_mfma.hip for 16 < m <= 128, blockinv_big.hip for fp64
-// 128 < m <= 256, the panel-blocked kernel up to 4096), 1 = the per-step register sweep, 5 = the
-// co-resident L2-image kernel (fp64 32 < m <= 128; GJ_BI_VARIANT=co), 6 = the per-step global
-// sweep for m > 256 instead of the panel-blocked kernel (reference timing)
+// 128 < m <= 256, the panel-blocked kernel up to 4096, the GPU-wide panel / GEMM form above),
+// 1 = the per-step register sweep, 5 = the co-resident L2-image kernel (fp64 32 < m <= 128;
+// GJ_BI_VARIANT=co), 6 = the per-step global sweep for m > 256 (reference timing), 7 = the GPU-wide
+// form for every m > 256 (GJ_BI_VARIANT=huge; tests)
 static int g_bi_variant = -1;
 int block_inverse_variant_id(const char* name) {
   const std::string v(name);
@@ -764,7 +765,8 @@ int block_inverse_variant_id(const char* name) {
   if (v == "sweep") return 1;
   if (v == "co") return 5;
   if (v == "generic") return 6;
-  throw std::invalid_argument("unknown block-inverse variant '" + v + "' (panel | sweep | co | generic)");
+  if (v == "huge") return 7;
+  throw std::invalid_argument("unknown block-inverse variant '" + v + "' (panel | sweep | co | generic | huge)");
 }
 static int bi_variant() {
   if (g_bi_variant < 0) {
@@ -808,7 +810,12 @@ static void launch_bi(const void* Lt, int64_t ldl, void* inv_t, double* scores, 
   else if (m <= 256 && sizeof(T) == 4)  // 256x256 fp32 = 64 VGPRs/lane at 1024 threads
     hipLaunchKernelGGL((block_inverse_kernel<T, 256, 1024>), dim3(grid), dim3(1024), 0, s, lt, ldl,
                        it, scores, valid, used, m, L.p, L.k, thresh, block_inverse_probe(), live_nblk);
-  else if (g_bi_variant != 6 && launch_blocked<T>(Lt, ldl, inv_t, scores, valid, used, L, thresh, nlive, s, scratch))
+  else if ((m > 4096 && g_bi_variant != 6) || (g_bi_variant == 7 && m > 256)) {
+    // m > 4096: the GPU-wide panel / GEMM form, one candidate at a time (blockinv_huge.hip)
+    block_inverse_huge(sizeof(T) == 8 ? DType::F64 : DType::F32, Lt, ldl, inv_t, scores, valid, used, L, thresh, s,
+                       scratch);
+    return;
+  } else if (g_bi_variant != 6 && launch_blocked<T>(Lt, ldl, inv_t, scores, valid, used, L, thresh, nlive, s, scratch))
     return;
   else
     hipLaunchKernelGGL((block_inverse_generic<T>), dim3(grid), dim3(256), 0, s, lt, ldl, it, scores,
@@ -823,6 +830,7 @@ const char* block_inverse_kernel_name(DType dt, int64_t m, int variant) {
   if (v == 0 && m > 16 && m <= 128) return "mfma_register";
   if (v != 1 && f64 && m > 128 && m <= 256) return "l2_image";
   if (m <= 128 || (m <= 256 && !f64)) return "register_sweep";
+  if ((m > 4096 && v != 6) || v == 7) return "gpu_panel_gemm";
   if (v != 6 && m <= 4096) return "panel_blocked";
   return "generic";
 }

@@ -4,6 +4,7 @@ import numpy as np
 import pytest
 import torch
 
+import mpi_jordan_crazy_acceleration_amd as gj
 from mpi_jordan_crazy_acceleration_amd import ops
 from mpi_jordan_crazy_acceleration_amd.utils import generate_matrix
 
@@ -124,6 +125,52 @@ def test_block_inverse(m, dtype, bi_variant):
         assert rel < tol, (b, rel)
         assert abs(scores[b].item() - np.abs(ref).sum(1).max()) / np.abs(ref).sum(1).max() < tol
     assert abs(scores[3].item() - 0.5) < 1e-6
+
+
+@pytest.mark.parametrize("m,dtype", [(300, torch.float64), (1000, torch.float64), (2500, torch.float64),
+                                     (700, torch.float32), (4608, torch.float64)])
+def test_block_inverse_huge_gpu_wide(native, m, dtype):
+    """The GPU-wide candidate inverse (panel factor on one workgroup + MFMA GEMM updates, the default
+    above m = 4096, forced with variant "huge" below): against numpy, with a singular block in the
+    batch, and against the panel-blocked kernel where that one applies (same pivot rule: inverses
+    and scores agree to rounding)."""
+    nblk = 3 if m <= 2500 else 2
+    rng = np.random.default_rng(m + 11)
+    W = rng.standard_normal((nblk, m, m))
+    if dtype == torch.float32:
+        W += np.sqrt(m) * np.eye(m)
+    W[1] = 0.0
+    X = W.reshape(nblk * m, m)
+    Lt = torch.from_numpy(-X.T.copy()).to(dtype).cuda()
+    native.set_block_inverse_variant("huge")
+    try:
+        inv_h, scores_h, valid_h = ops.block_inverse(Lt, nblk * m, m, 1, 0, thresh=1e-12)
+    finally:
+        native.set_block_inverse_variant("panel")
+    assert valid_h.cpu().tolist()[:2] == [1, 0]
+    tol = 1e-9 if dtype == torch.float64 else 1e-4
+    for b in [x for x in range(nblk) if x != 1]:
+        ref = np.linalg.inv(W[b].astype(np.float32 if dtype == torch.float32 else np.float64).astype(np.float64))
+        got = inv_h[b].cpu().double().numpy().T
+        assert np.abs(got - ref).max() / np.abs(ref).max() < tol
+        assert abs(scores_h[b].item() / np.abs(ref).sum(1).max() - 1) < tol * 10
+    if m <= 4096:  # the panel-blocked kernel (or the matrix-core one) on the same batch
+        inv_p, scores_p, valid_p = ops.block_inverse(Lt, nblk * m, m, 1, 0, thresh=1e-12)
+        assert valid_p.cpu().tolist() == valid_h.cpu().tolist()
+        for b in (0, 2):
+            a, c = inv_h[b].cpu().double(), inv_p[b].cpu().double()
+            assert ((a - c).abs().max() / c.abs().max()).item() < tol
+            assert abs(scores_h[b].item() / scores_p[b].item() - 1) < tol * 10
+
+
+@pytest.mark.parametrize("n,m", [(5000, 5000), (9000, 4500)])
+def test_engine_block_size_above_4096(n, m):
+    """m > 4096 in the solver (the reference inverts any m, main.cpp:746-820): one or two block rows,
+    every candidate inverse on the GPU-wide path; the inverse against numpy."""
+    A = generate_matrix(n, "random", 23)
+    inv = gj.GaussJordan(block_size=m, ranks=1, device="gpu").inverse(A)
+    ref = np.linalg.inv(A)
+    assert np.abs(inv - ref).max() / np.abs(ref).max() < 1e-8 * max(1.0, m / 256)
 
 
 @pytest.mark.parametrize("m,dtype", [(2500, torch.float64), (4096, torch.float32)])
@@ -447,7 +494,9 @@ def _reference_pivots(W):
     (1000, torch.float64, "panel"),
     # the register sweep kernel: default for m <= 16 and fp32 128 < m <= 256, variant "sweep" else
     (16, torch.float64, "panel"), (200, torch.float32, "panel"), (128, torch.float64, "sweep"),
-    (60, torch.float32, "sweep")])
+    (60, torch.float32, "sweep"),
+    # the GPU-wide panel / GEMM form (m > 4096 by default; forced here)
+    (300, torch.float64, "huge"), (700, torch.float32, "huge")])
 def test_block_inverse_pivot_rule(native, m, dtype, variant):
     """exact magnitudes (ties resolved in the low word of the fp64 key) and, on
     equal magnitudes, the row at the lowest CURRENT position under the reference's swaps — in
