@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Latency of the batched candidate-block inversion (pivot search) in isolation (device-side events).
 
-    [BI_M="64 128"] [BI_NBLK="8 32 64 256"] python bench/bench_blockinv.py [panel] [sweep] [co] [generic]
+    [BI_M="64 128"] [BI_NBLK="8 32 64 256"] [BI_REPS=50] python bench/bench_blockinv.py [panel] [sweep] [co] [generic] [huge]
 """
 import json
 import os
@@ -28,7 +28,7 @@ def main(variants):
                     # device-side: 50 back-to-back launches between two events
                     us = ops.device_for(Lt).time_block_inverse(
                         ops._DT[dt], Lt.data_ptr(), Lt.stride(0), inv_t.data_ptr(), scores.data_ptr(),
-                        valid.data_ptr(), used.data_ptr(), n, m, 1, 0, 0.0, 50)
+                        valid.data_ptr(), used.data_ptr(), n, m, 1, 0, 0.0, int(os.environ.get("BI_REPS", "50")))
                     print(json.dumps({"variant": var, "m": m, "nblk": nblk, "dtype": str(dt).split(".")[-1],
                                       "us_per_call": round(us, 1), "us_per_step": round(us / m, 3)}), flush=True)
     C.set_block_inverse_variant("panel")

@@ -757,7 +757,8 @@ static bool launch_blocked(const void* Lt, int64_t ldl, void* inv_t, double* sco
 // 128 < m <= 256, the panel-blocked kernel up to 4096, the GPU-wide panel / GEMM form above),
 // 1 = the per-step register sweep, 5 = the co-resident L2-image kernel (fp64 32 < m <= 128;
 // GJ_BI_VARIANT=co), 6 = the per-step global sweep for m > 256 (reference timing), 7 = the GPU-wide
-// form for every m > 256 (GJ_BI_VARIANT=huge; tests)
+// form for every m > 256 (GJ_BI_VARIANT=huge; tests), 8 = the panel-blocked kernel for every
+// 256 < m <= 4096 whatever the live count (GJ_BI_VARIANT=blocked; tests)
 static int g_bi_variant = -1;
 int block_inverse_variant_id(const char* name) {
   const std::string v(name);
@@ -766,7 +767,8 @@ int block_inverse_variant_id(const char* name) {
   if (v == "co") return 5;
   if (v == "generic") return 6;
   if (v == "huge") return 7;
-  throw std::invalid_argument("unknown block-inverse variant '" + v + "' (panel | sweep | co | generic | huge)");
+  if (v == "blocked") return 8;
+  throw std::invalid_argument("unknown block-inverse variant '" + v + "' (panel | sweep | co | generic | huge | blocked)");
 }
 static int bi_variant() {
   if (g_bi_variant < 0) {
@@ -777,6 +779,18 @@ static int bi_variant() {
 }
 void set_block_inverse_variant(int v) { g_bi_variant = v; }
 int block_inverse_variant() { return bi_variant(); }
+
+// The GPU-wide form (one candidate at a time, every CU) against the panel-blocked kernel (every
+// candidate at once, one workgroup each), by the live candidate count: per batch, measured
+// (scripts/runs/r6_bi_large.sh, fp64, ms) panel 6.7 / 43 / 578 / 8160 at m = 512 / 1024 / 2048 /
+// 4096 whatever the count, GPU-wide 4.7 / 12.5 / 41 / 150 per candidate.
+static bool huge_preferred(int64_t m, int64_t nlive) {
+  if (m > 4096) return true;
+  if (m > 2048) return nlive <= 48;
+  if (m > 1536) return nlive <= 12;
+  if (m >= 1024) return nlive <= 3;
+  return false;
+}
 
 template <typename T>
 static void launch_bi(const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,
@@ -810,8 +824,10 @@ static void launch_bi(const void* Lt, int64_t ldl, void* inv_t, double* scores, 
   else if (m <= 256 && sizeof(T) == 4)  // 256x256 fp32 = 64 VGPRs/lane at 1024 threads
     hipLaunchKernelGGL((block_inverse_kernel<T, 256, 1024>), dim3(grid), dim3(1024), 0, s, lt, ldl,
                        it, scores, valid, used, m, L.p, L.k, thresh, block_inverse_probe(), live_nblk);
-  else if ((m > 4096 && g_bi_variant != 6) || (g_bi_variant == 7 && m > 256)) {
-    // m > 4096: the GPU-wide panel / GEMM form, one candidate at a time (blockinv_huge.hip)
+  else if ((m > 4096 && g_bi_variant != 6) || (g_bi_variant == 0 && huge_preferred(m, nlive >= 0 ? nlive : L.nblk)) ||
+           (g_bi_variant == 7 && m > 256)) {
+    // large m, few live candidates: the GPU-wide panel / GEMM form, one candidate at a time
+    // (blockinv_huge.hip)
     block_inverse_huge(sizeof(T) == 8 ? DType::F64 : DType::F32, Lt, ldl, inv_t, scores, valid, used, L, thresh, s,
                        scratch);
     return;
@@ -831,6 +847,7 @@ const char* block_inverse_kernel_name(DType dt, int64_t m, int variant) {
   if (v != 1 && f64 && m > 128 && m <= 256) return "l2_image";
   if (m <= 128 || (m <= 256 && !f64)) return "register_sweep";
   if ((m > 4096 && v != 6) || v == 7) return "gpu_panel_gemm";
+  if (v == 0 && m >= 1024) return "panel_blocked|gpu_panel_gemm (by live candidates)";
   if (v != 6 && m <= 4096) return "panel_blocked";
   return "generic";
 }
