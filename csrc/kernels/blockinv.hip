@@ -828,8 +828,8 @@ static void launch_bi(const void* Lt, int64_t ldl, void* inv_t, double* scores, 
            (g_bi_variant == 7 && m > 256)) {
     // large m, few live candidates: the GPU-wide panel / GEMM form, one candidate at a time
     // (blockinv_huge.hip)
-    block_inverse_huge(sizeof(T) == 8 ? DType::F64 : DType::F32, Lt, ldl, inv_t, scores, valid, used, L, thresh, s,
-                       scratch);
+    block_inverse_huge(sizeof(T) == 8 ? DType::F64 : DType::F32, Lt, ldl, inv_t, scores, valid, used, L, thresh,
+                       nlive, s, scratch);
     return;
   } else if (g_bi_variant != 6 && launch_blocked<T>(Lt, ldl, inv_t, scores, valid, used, L, thresh, nlive, s, scratch))
     return;

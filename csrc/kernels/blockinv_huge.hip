@@ -251,9 +251,13 @@ unsigned grid_of(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int
 
 }  // namespace
 
+// touch_used = false (the engine's live-candidate launch, nlive >= 0): a used block's score, flag and
+// inverse are left as they are, like the one-workgroup-per-live-candidate kernels; true (one launch
+// per block): they are set to 0, like block_inverse_generic.
 template <typename T>
 static void huge_launch(const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,
-                        const int32_t* used, const Layout& L, double thresh, hipStream_t s, void* scratch) {
+                        const int32_t* used, const Layout& L, double thresh, hipStream_t s, void* scratch,
+                        bool touch_used) {
   const int m = (int)L.m;
   const int64_t nblk = L.nblk;
   const int nparts = (m + 255) / 256;
@@ -287,6 +291,7 @@ static void huge_launch(const void* Lt, int64_t ldl, void* inv_t, double* scores
     T* Wc = static_cast<T*>(scratch) + b * (int64_t)m * m;
     T* out = static_cast<T*>(inv_t) + b * (int64_t)m * m;
     const int is_used = g_huge.host_used[b] != 0;
+    if (is_used && !touch_used) continue;
     hipLaunchKernelGGL((huge_init<T>), dim3(grid_of((int64_t)m * m)), dim3(256), 0, s, lt, ldl, Wc, m, (int)b, is_used,
                        ib);
     if (!is_used) {
@@ -314,12 +319,13 @@ static void huge_launch(const void* Lt, int64_t ldl, void* inv_t, double* scores
 }
 
 void block_inverse_huge(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,
-                        const int32_t* used, const Layout& L, double thresh, hipStream_t s, void* scratch) {
+                        const int32_t* used, const Layout& L, double thresh, int64_t nlive, hipStream_t s,
+                        void* scratch) {
   if (L.nblk <= 0) return;
   if (dt == DType::F64)
-    huge_launch<double>(Lt, ldl, inv_t, scores, valid, used, L, thresh, s, scratch);
+    huge_launch<double>(Lt, ldl, inv_t, scores, valid, used, L, thresh, s, scratch, nlive < 0);
   else
-    huge_launch<float>(Lt, ldl, inv_t, scores, valid, used, L, thresh, s, scratch);
+    huge_launch<float>(Lt, ldl, inv_t, scores, valid, used, L, thresh, s, scratch, nlive < 0);
 }
 
 }  // namespace kern

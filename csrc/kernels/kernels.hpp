@@ -67,7 +67,8 @@ size_t block_inverse_big_scratch_bytes(DType dt, const Layout& L);
 // blockinv_huge.hip: m > 4096 (or GJ_BI_VARIANT=huge), one candidate at a time with the whole GPU
 // (panel factor + MFMA GEMM updates); scratch: nblk m x m slabs (the generic path's)
 void block_inverse_huge(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,
-                        const int32_t* used, const Layout& L, double thresh, hipStream_t s, void* scratch);
+                        const int32_t* used, const Layout& L, double thresh, int64_t nlive, hipStream_t s,
+                        void* scratch);
 // the co-resident form (4 waves, fits the slot one trailing-update workgroup frees): fp64 32 < m <= 128;
 // with sel, the batch's last workgroup also runs the selection (as block_inverse_mfma)
 bool block_inverse_co(DType dt, const void* Lt, int64_t ldl, void* inv_t, double* scores, int32_t* valid,

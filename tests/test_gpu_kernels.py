@@ -686,7 +686,8 @@ def test_pivot_select_single_bookkeeping(native):
                                              ("panel", 100, torch.float32), ("co", 128, torch.float64),
                                              ("panel", 256, torch.float64), ("panel", 300, torch.float64),
                                              ("panel", 1100, torch.float64), ("panel", 1700, torch.float32),
-                                             ("sweep", 64, torch.float64), ("generic", 300, torch.float64)])
+                                             ("sweep", 64, torch.float64), ("generic", 300, torch.float64),
+                                             ("huge", 600, torch.float64)])
 @pytest.mark.parametrize("p,k", [(1, 0), (3, 2)])
 def test_block_inverse_live_grid_matches_full_grid(native, variant, m, dtype, p, k):
     """nlive >= 0 (the engine's launch): one workgroup per UNUSED candidate, the workgroup's block
