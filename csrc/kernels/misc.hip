@@ -574,11 +574,55 @@ __global__ __launch_bounds__(256) void permute_kernel(T* __restrict__ dst, int64
   }
 }
 
+// 16-byte form: each thread moves UNR vectors per trip, all loads issued before the stores (the
+// scalar form above held one 8-byte load in flight per thread: N = 32768 fp64 3.9 ms = 4.4 TB/s,
+// N = 8192 308 us).  vpb = 16-byte vectors per column block.
+template <int UNR>
+__global__ __launch_bounds__(256) void permute_vec_kernel(uint4* __restrict__ dst, int64_t ldd4,
+                                                          const uint4* __restrict__ X, int64_t ldx4,
+                                                          int m, unsigned vpb, unsigned nvec,
+                                                          const int32_t* dst_blk, const int32_t* colsrc) {
+  const int64_t row = blockIdx.x;
+  const int64_t b = row / m, r = row - b * m;
+  uint4* d = dst + ((int64_t)dst_blk[b] * m + r) * ldd4;
+  const uint4* s = X + row * ldx4;
+  const unsigned stride = gridDim.y * 256u;
+  for (unsigned i0 = blockIdx.y * 256u + threadIdx.x; i0 < nvec; i0 += stride * UNR) {
+    uint4 v[UNR];
+    unsigned at[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const unsigned i = i0 + (unsigned)u * stride;
+      at[u] = i;
+      if (i < nvec) {
+        const unsigned c = i / vpb, j = i - c * vpb;
+        v[u] = s[(int64_t)colsrc[c] * vpb + j];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+      if (at[u] < nvec) d[at[u]] = v[u];
+  }
+}
+
 void permute_blocks(DType dt, void* dst, int64_t ldd, const void* X, int64_t ldx, int64_t nblk,
                     int64_t m, int64_t Nr, const int32_t* dst_blk, const int32_t* colsrc,
                     hipStream_t s) {
   if (nblk <= 0) return;
   const int64_t ncols = Nr * m;
+  const int64_t es = dt == DType::F64 ? 8 : 4;
+  const bool aligned = (m * es) % 16 == 0 && (ldd * es) % 16 == 0 && (ldx * es) % 16 == 0 &&
+                       (reinterpret_cast<uintptr_t>(dst) % 16) == 0 && (reinterpret_cast<uintptr_t>(X) % 16) == 0 &&
+                       ncols * es / 16 < (int64_t(1) << 31);
+  if (aligned) {
+    constexpr int kUnr = 4;
+    const unsigned vpb = (unsigned)(m * es / 16), nvec = (unsigned)(ncols * es / 16);
+    const unsigned gy = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nvec + 256 * kUnr - 1) / (256 * kUnr), 64));
+    hipLaunchKernelGGL(permute_vec_kernel<kUnr>, dim3((unsigned)(nblk * m), gy), dim3(256), 0, s,
+                       static_cast<uint4*>(dst), ldd * es / 16, static_cast<const uint4*>(X), ldx * es / 16, (int)m,
+                       vpb, nvec, dst_blk, colsrc);
+    return;
+  }
   const int64_t per = std::max<int64_t>(1, 256 / m);
   const unsigned gy = (unsigned)std::min<int64_t>((Nr + per * 4 - 1) / (per * 4), 64);
   dim3 grid((unsigned)(nblk * m), gy);

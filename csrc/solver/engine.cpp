@@ -118,9 +118,25 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
     target_cols = std::max<int64_t>((L_.npad + 7) / 8, std::min<int64_t>(8192, (L_.npad + 1) / 2));
   int64_t cw = std::max<int64_t>(1, target_cols / m);
   cw = ((cw + d_ - 1) / d_) * d_;
-  for (int64_t b = 0; b < L_.Nr; b += cw) {
-    cb0_.push_back(b);
-    cb1_.push_back(std::min(L_.Nr, b + cw));
+  if (const char* e = std::getenv("GJ_CHUNK_PLAN")) {
+    // explicit plan for A/B runs: comma-separated block counts, each a multiple of d, summing to Nr
+    int64_t b = 0;
+    for (const char* s = e; *s;) {
+      char* end = nullptr;
+      const int64_t w = std::strtoll(s, &end, 10);
+      GJ_REQUIRE(end != s && w > 0 && w % d_ == 0, "GJ_CHUNK_PLAN: block counts must be positive multiples of the depth");
+      cb0_.push_back(b);
+      cb1_.push_back(b + w);
+      b += w;
+      s = (*end == ',') ? end + 1 : end;
+      GJ_REQUIRE(*end == ',' || *end == 0, "GJ_CHUNK_PLAN: expected a comma-separated list");
+    }
+    GJ_REQUIRE(b == L_.Nr, "GJ_CHUNK_PLAN: block counts must sum to the number of block columns");
+  } else {
+    for (int64_t b = 0; b < L_.Nr; b += cw) {
+      cb0_.push_back(b);
+      cb1_.push_back(std::min(L_.Nr, b + cw));
+    }
   }
   chunk_of_.resize(L_.Nr);
   for (size_t c = 0; c < cb0_.size(); ++c)

@@ -243,10 +243,13 @@ def _row_blocks_case(m, blocks, latency, c_in, dtype):
     assert torch.equal(T[:, sel], Tf[:, sel]) and bool((T[:, ~sel] == 5.0).all())
 
 
-@pytest.mark.parametrize("m", [32, 60, 128, 300])
-def test_permute_blocks(m):
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("m", [32, 33, 60, 128, 300])
+def test_permute_blocks(m, dtype):
+    # the 16-byte kernel where a column block's bytes and the leading dimensions are multiples of 16
+    # (every m here but 33), the scalar one otherwise
     nblk, Nr = 3, 5
-    X = _rand((nblk * m, Nr * m), torch.float64, 9).cuda()
+    X = _rand((nblk * m, Nr * m), dtype, 9).cuda()
     dst = torch.tensor([2, 0, 1], dtype=torch.int32, device="cuda")
     colsrc = torch.tensor([4, 3, 0, 1, 2], dtype=torch.int32, device="cuda")
     out = ops.permute_blocks(X, m, dst, colsrc).cpu()

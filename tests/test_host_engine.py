@@ -108,6 +108,19 @@ def test_chunking_does_not_change_result():
     assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("ranks", [1, 2])
+def test_uneven_chunk_plan_does_not_change_result(monkeypatch, ranks):
+    # GJ_CHUNK_PLAN: explicit, uneven column chunks (block counts; multiples of the depth)
+    A = _mat("rand", 160, 9)
+    a = gj.GaussJordan(block_size=8, ranks=ranks, device="cpu", depth=2).inverse(A)
+    monkeypatch.setenv("GJ_CHUNK_PLAN", "6,10,4")
+    b = gj.GaussJordan(block_size=8, ranks=ranks, device="cpu", depth=2).inverse(A)
+    assert np.array_equal(a, b)
+    monkeypatch.setenv("GJ_CHUNK_PLAN", "6,10,5")
+    with pytest.raises(Exception, match="GJ_CHUNK_PLAN"):
+        gj.GaussJordan(block_size=8, ranks=ranks, device="cpu", depth=2).inverse(A)
+
+
 def test_solve_rhs():
     A = _mat("rand", 64, 11)
     x = np.arange(64.0)
