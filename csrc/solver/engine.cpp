@@ -268,9 +268,13 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // chunk pass) where CUs are reserved for the chain (scripts/runs/r5_skip.sh, r5_skip2.sh): N = 8192
   // 24.20 -> 23.61 ms, N = 16384 151.5 -> 150.3 ms, emulated p = 8 at N = 16384 -3 %; without a
   // reservation (N = 32768) the MAIN merge measured +0.1-0.3 % and the chunk-pass merge +1.5 %.
-  skip_cols_ = reserved_cus_ > 0;
+  // Round 6, 128 x 128 tile (3 per CU, twice the work per tile: a split chunk's two launch tails
+  // cost more): the MAIN merge at N = 32768 1078.2 / 1079.5 -> 1076.3 / 1075.5 ms, same box,
+  // alternating (scripts/runs/r6_skip128.sh) -- on wherever that tile runs; the chunk-pass merge
+  // stays with the reservation.
+  skip_cols_ = reserved_cus_ > 0 || gemm_tile_ == 128;
   if (const char* e = std::getenv("GJ_SKIP_COLS")) skip_cols_ = std::atoi(e) != 0;
-  chunk_skip_ = skip_cols_;
+  chunk_skip_ = reserved_cus_ > 0;
   // the chain's latency GEMMs on the register-fed small kernel where CUs are reserved for it
   // (scripts/runs/r5_latk.sh): N = 8192 23.42 -> 22.80 ms, emulated p = 8 at N = 32768 -1.5 / -3.7 %
   // (comm-free / direct 50 GB/s), p = 4 at N = 16384 -4 %; N = 16384 even
