@@ -220,6 +220,7 @@ class Engine {
     bool skip_cols = false;       // one MAIN launch per chunk around the look-ahead columns (skip_cols_)
     bool lat_reg = false;         // the chain's latency GEMMs on the register-fed kernel (lat_reg_)
     bool chunk_skip = false;      // one chunk-pass launch per step around the panel columns (chunk_skip_)
+    int first_depth = 0;          // steps of the first panel (f_)
   };
   Policy policy() const;
   const std::string& bcast_algo() const { return bcast_algo_; }  // "ring" | "direct"
@@ -303,9 +304,12 @@ class Engine {
   void prof_collect(SolveStats& st);
   size_t esz() const { return dtype_size(opt_.dtype); }
   char* elem(void* base, int64_t off) const { return static_cast<char*>(base) + off * (int64_t)esz(); }
-  int64_t panel_t0(int64_t v) const { return v * d_; }
-  int64_t panel_q(int64_t v) const { return std::min<int64_t>(d_, L_.Nr - v * d_); }
-  int64_t npanels() const { return (L_.Nr + d_ - 1) / d_; }
+  // panel 0 is f_ steps deep (a shorter prologue before MAIN's first update), every later one d_
+  int64_t panel_t0(int64_t v) const { return v == 0 ? 0 : f_ + (v - 1) * d_; }
+  int64_t panel_q(int64_t v) const { return std::min<int64_t>(v == 0 ? f_ : d_, L_.Nr - panel_t0(v)); }
+  int64_t npanels() const { return L_.Nr <= f_ ? 1 : 1 + (L_.Nr - f_ + d_ - 1) / d_; }
+  int64_t panel_of(int64_t t) const { return t < f_ ? 0 : 1 + (t - f_) / d_; }
+  bool panel_boundary(int64_t b) const { return b == 0 || b >= L_.Nr || (b >= f_ && (b - f_) % d_ == 0); }
   // chunk c of the stacked-rows buffer: (d*m) x W block, ld W
   char* rb_chunk(int par, int64_t c) const {
     return elem(Rb_[par], (int64_t)d_ * L_.m * cb0_[c] * L_.m);
@@ -318,6 +322,7 @@ class Engine {
   SolveOptions opt_;
   Layout L_;
   int d_ = 1;
+  int f_ = 1;  // depth of the first panel (GJ_FIRST_DEPTH; default d_)
   std::string bcast_algo_ = "ring";
   bool comm_small_tiles_ = false;  // COMM chunk-normalisation GEMMs on the small latency tile
   int bi_hint_ = -1;               // candidate-inverse kernel family (Device::set_block_inverse_hint)

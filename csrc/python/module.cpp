@@ -510,6 +510,7 @@ PYBIND11_MODULE(_C, mod) {
                                d["skip_cols"] = pl.skip_cols;
                                d["lat_reg"] = pl.lat_reg;
                                d["chunk_skip"] = pl.chunk_skip;
+                               d["first_depth"] = pl.first_depth;
                                d["bcast"] = e.eng->bcast_algo();
                                d["bcast_tuning"] = e.comm->bcast_report();
                                d["comm"] = e.comm->describe();

@@ -109,6 +109,9 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
                    : (L_.p == 1 && L_.npad <= 8192) ? 2
                    : (small_rank && L_.npad > 16384) ? 8 : 4;
   d_ = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)want, (int64_t)kMaxDepth, L_.Nr}));
+  f_ = d_;
+  if (const char* e = std::getenv("GJ_FIRST_DEPTH"))
+    if (std::atoi(e) > 0) f_ = (int)std::min<int64_t>({(int64_t)std::atoi(e), (int64_t)d_, L_.Nr});
 
   // Column chunk plan: fixed partition of the Nr block columns into runs of a multiple of d blocks.
   int64_t target_cols = opt_.chunk_cols;
@@ -118,13 +121,16 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
     target_cols = std::max<int64_t>((L_.npad + 7) / 8, std::min<int64_t>(8192, (L_.npad + 1) / 2));
   int64_t cw = std::max<int64_t>(1, target_cols / m);
   cw = ((cw + d_ - 1) / d_) * d_;
+  // (chunk boundaries sit on panel boundaries: with a shallower first panel, at f_ + k d_ -- the
+  // first chunk f_ blocks wider)
   if (const char* e = std::getenv("GJ_CHUNK_PLAN")) {
     // explicit plan for A/B runs: comma-separated block counts, each a multiple of d, summing to Nr
     int64_t b = 0;
     for (const char* s = e; *s;) {
       char* end = nullptr;
       const int64_t w = std::strtoll(s, &end, 10);
-      GJ_REQUIRE(end != s && w > 0 && w % d_ == 0, "GJ_CHUNK_PLAN: block counts must be positive multiples of the depth");
+      GJ_REQUIRE(end != s && w > 0 && panel_boundary(b + w),
+                 "GJ_CHUNK_PLAN: block counts must end on panel boundaries (multiples of the depth)");
       cb0_.push_back(b);
       cb1_.push_back(b + w);
       b += w;
@@ -133,9 +139,11 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
     }
     GJ_REQUIRE(b == L_.Nr, "GJ_CHUNK_PLAN: block counts must sum to the number of block columns");
   } else {
-    for (int64_t b = 0; b < L_.Nr; b += cw) {
+    for (int64_t b = 0; b < L_.Nr;) {
+      const int64_t e = std::min(L_.Nr, b == 0 ? cw + (f_ < d_ ? f_ : 0) : b + cw);
       cb0_.push_back(b);
-      cb1_.push_back(std::min(L_.Nr, b + cw));
+      cb1_.push_back(e);
+      b = e;
     }
   }
   chunk_of_.resize(L_.Nr);
@@ -169,8 +177,8 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   gemm_tile_ = (reserved_cus_ == 0 && L_.max_nblk * L_.m > 8192) ? 128 : 64;
   dev_.set_gemm_tile_hint(gemm_tile_);
   if (const char* e = std::getenv("GJ_DENSE_GEMM")) dense_gemm_ = std::atoi(e) != 0;
-  // Candidate inverses on ranks whose trailing update holds every CU (p > 1 without a reservation:
-  // the 16384- and 8192-row ranks of N = 32768) take the co-resident 4-wave form, which starts in
+  // (Rounds 2-5) candidate inverses on ranks whose trailing update holds every CU (p > 1 without a
+  // reservation: the 16384- and 8192-row ranks of N = 32768) took the co-resident 4-wave form, which starts in
   // the slot one retiring trailing-update workgroup frees instead of waiting for a whole CU: the
   // p = 4 rank spends 616 of its 1154 us per step in a block inverse that alone takes ~100 us
   // (profiles/rocprof_emu4_r2.md).  Rank-0 emulation at N = 32768, 100 GB/s model: p = 2 0.585 ->
@@ -179,7 +187,12 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // overrides; an explicit process-wide GJ_BI_VARIANT wins.
   {
     const bool fits = opt_.dtype == DType::F64 && L_.m > 32 && L_.m <= 128;
-    bool co = dev_.on_gpu() && L_.p > 1 && rc == 0;
+    // Round 6, on the 2-stage 128 x 128 / 3-stage 128 x 64 trailing-update tiles: the register form
+    // is faster on those ranks too (scripts/runs/r6_emuco.sh, emulated N = 32768, two repetitions:
+    // p = 2 0.5305 / 0.5313 -> 0.5258 / 0.5275 s comm-free, p = 4 0.2740 / 0.2741 -> 0.2717 / 0.2721
+    // s, direct 50 GB/s 0.2866 / 0.2873 -> 0.2776 / 0.2776 s; one GPU, profiles/blockinv_coresident.md):
+    // the co-resident form is opt-in (GJ_BI_CORESIDENT=1).
+    bool co = false;
     if (const char* e = std::getenv("GJ_BI_CORESIDENT")) co = std::atoi(e) != 0;
     if (std::getenv("GJ_BI_VARIANT")) co = false;
     bi_hint_ = (co && fits) ? 5 : -1;
@@ -310,6 +323,7 @@ Engine::~Engine() {
 Engine::Policy Engine::policy() const {
   Policy p;
   p.depth = d_;
+  p.first_depth = f_;
   p.env_overrides = env_overrides_;
   p.gemm_tile = gemm_tile_;
   p.nchunks = (int)cb0_.size();
@@ -774,7 +788,7 @@ void Engine::select(int64_t t, const void* Lt, bool full) {
   dev_.pivot_global(L_.p > 1 ? recs_ : myrec_, (int32_t)L_.p, (int32_t)t, pos_, phys_at_, used_, seq_, piv_dev_,
                     &piv_host_[par], S_SIDE);
   if (vparts_ && L_.p > 1)  // the gathered records every rank just reduced identically
-    vhash(t / d_, vslot(V_RECS, t % d_), recs_, (int64_t)sizeof(PivotRec) * L_.p, (int64_t)sizeof(PivotRec) * L_.p,
+    vhash(panel_of(t), vslot(V_RECS, t - panel_t0(panel_of(t))), recs_, (int64_t)sizeof(PivotRec) * L_.p, (int64_t)sizeof(PivotRec) * L_.p,
           1, S_SIDE);
   prof_end(PH_EXCHANGE, pe, S_SIDE);
   dbg_sync();

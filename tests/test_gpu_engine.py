@@ -238,9 +238,8 @@ def test_async_ranks_direct_bcast_on_one_gpu(p, monkeypatch):
 def test_async_ranks_driver_shapes(p, bcast, monkeypatch):
     """The engine configurations the multi-GPU scaling run gets, on p stream-ordered virtual ranks of
     one GPU with random arrival delays: p = 8 (ranks of <= 4096 rows of an order above 16384:
-    depth-8 panels, 32 reserved CUs, 8192-column chunks) and p = 2 / 3 (no reservation: the
-    co-resident candidate inverse), both broadcast algorithms.  The residual must match the
-    single-GPU solve of the same matrix."""
+    depth-8 panels, 32 reserved CUs, 8192-column chunks) and p = 2 / 3 (no reservation), both
+    broadcast algorithms.  The residual must match the single-GPU solve of the same matrix."""
     monkeypatch.setenv("GJ_BCAST", bcast)
     n, m = 16512, 128
     one = gj.GaussJordan(block_size=m, ranks=1, device="gpu").run(n, gen="random", seed=3)
@@ -280,11 +279,12 @@ def test_depth2_p8_async_jittered(n):
     assert rep["residual"] < 10 * one["residual"] + 1e-9, (rep["residual"], one["residual"])
 
 
-@pytest.mark.parametrize("p", [1, 4])
-def test_race_check_on_gpu(p):
+@pytest.mark.parametrize("p,co", [(1, "0"), (4, "0"), (4, "1")])
+def test_race_check_on_gpu(p, co, monkeypatch):
     """The schedule checker around the HIP device: the GPU's op sequence (fused candidate inverse +
-    selection, CU reservation, co-resident candidate inverse at p > 1, tuned broadcast) is race-free
-    and the wrapped run still computes the right inverse."""
+    selection, CU reservation, the opt-in co-resident candidate inverse at p > 1, tuned broadcast) is
+    race-free and the wrapped run still computes the right inverse."""
+    monkeypatch.setenv("GJ_BI_CORESIDENT", co)
     rep = gj.GaussJordan(block_size=64, ranks=p, device="gpu", comm="async" if p > 1 else "auto",
                          race_check=True, jitter_us=20.0).run(1500, gen="random", seed=2)
     assert rep["status"] == 0, rep["message"]

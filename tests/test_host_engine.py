@@ -254,3 +254,31 @@ def test_unknown_variant_names_fail_loudly(native):
         native.set_block_inverse_variant("pannel")
     native.set_gemm_variant("auto")
     native.set_block_inverse_variant("panel")
+
+
+@pytest.mark.parametrize("first", [1, 2, 3])
+@pytest.mark.parametrize("depth", [2, 4, 6])
+@pytest.mark.parametrize("n,m,p", [(37, 5, 1), (37, 5, 3), (64, 8, 2), (50, 7, 5), (12, 12, 2)])
+def test_shallow_first_panel_matches_numpy(monkeypatch, first, depth, n, m, p):
+    # GJ_FIRST_DEPTH: panel 0 takes `first` steps (capped at the depth), every later one `depth`;
+    # chunk boundaries move onto the shifted panel boundaries; GJ_VERIFY checks every hand-over
+    monkeypatch.setenv("GJ_FIRST_DEPTH", str(first))
+    monkeypatch.setenv("GJ_VERIFY", "1")
+    A = _mat("perm", n, seed=n + m + p + first)
+    g = gj.GaussJordan(block_size=m, ranks=p, device="cpu", depth=depth, chunk_cols=2 * m)
+    inv = g.inverse(A)
+    ref = np.linalg.inv(A)
+    assert np.abs(inv - ref).max() / np.abs(ref).max() < 1e-10
+
+
+def test_shallow_first_panel_chunk_plan(monkeypatch):
+    # explicit plans must end on the shifted panel boundaries (1 + 2k for first depth 1, depth 2)
+    A = _mat("rand", 160, 9)
+    ref = np.linalg.inv(A)
+    monkeypatch.setenv("GJ_FIRST_DEPTH", "1")
+    monkeypatch.setenv("GJ_CHUNK_PLAN", "7,10,3")
+    inv = gj.GaussJordan(block_size=8, device="cpu", depth=2).inverse(A)
+    assert np.abs(inv - ref).max() / np.abs(ref).max() < 1e-10
+    monkeypatch.setenv("GJ_CHUNK_PLAN", "6,10,4")
+    with pytest.raises(Exception, match="GJ_CHUNK_PLAN"):
+        gj.GaussJordan(block_size=8, device="cpu", depth=2).inverse(A)
