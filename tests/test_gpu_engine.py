@@ -324,3 +324,20 @@ def test_generated_norm_matches_uploaded(native, dtype, gen):
     su = u.solve()
     assert sg["status"] == su["status"]
     assert g.input_norm_inf() == u.input_norm_inf() == pytest.approx(np.abs(A).sum(1).max(), rel=1e-6)
+
+
+@pytest.mark.parametrize("p,first,plan", [(1, "1", ""), (1, "1", "9,16,7"), (3, "2", ""), (4, "1", "")])
+def test_async_first_depth_and_chunk_plan_on_gpu(p, first, plan, monkeypatch):
+    """GJ_FIRST_DEPTH (a shallower panel 0, chunk boundaries on the shifted panel boundaries) and an
+    explicit uneven GJ_CHUNK_PLAN on the GPU, one rank and stream-ordered virtual ranks (verify on):
+    the residual must match the default schedule's."""
+    n, m = 4096, 128  # 32 block columns; depth 4 at p > 1, 2 at p = 1
+    base = gj.GaussJordan(block_size=m, ranks=p, device="gpu", comm="async" if p > 1 else "auto").run(
+        n, gen="random", seed=5)
+    monkeypatch.setenv("GJ_FIRST_DEPTH", first)
+    if plan:
+        monkeypatch.setenv("GJ_CHUNK_PLAN", plan)
+    rep = gj.GaussJordan(block_size=m, ranks=p, device="gpu", comm="async" if p > 1 else "auto",
+                         jitter_us=20.0 if p > 1 else 0.0).run(n, gen="random", seed=5)
+    assert base["status"] == 0 and rep["status"] == 0, (base["message"], rep["message"])
+    assert rep["residual"] < 10 * base["residual"] + 1e-9, (rep["residual"], base["residual"])
