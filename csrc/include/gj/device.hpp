@@ -75,6 +75,9 @@ struct GemmExtra {
   int glds_build = 0;
   // This launch's LDS-DMA tile width (64 | 128), 0 = the device's hint (Device::set_gemm_tile_hint)
   int glds_tile = 0;
+  // fp64 LDS-DMA kernel: C read (bit 0) / written (bit 1) with the non-temporal cache policy, for C
+  // that nothing reads again soon (MAIN's trailing update: Engine::main_cnt_); -1 = GJ_GLDS_CNT / 0
+  int c_nt = -1;
   // Row-block selection (the pivot-chain / deferred split of a panel's column updates, Engine):
   // only the row blocks b (height rsel_m, b < 64 kRselWords) whose bit b of rsel is set take part;
   // M counts the selected rows ((set bits) * rsel_m) and the i-th block of M is the i-th set bit.

@@ -221,6 +221,7 @@ class Engine {
     bool lat_reg = false;         // the chain's latency GEMMs on the register-fed kernel (lat_reg_)
     bool chunk_skip = false;      // one chunk-pass launch per step around the panel columns (chunk_skip_)
     int first_depth = 0;          // steps of the first panel (f_)
+    int main_cnt = 0;             // MAIN's C tile non-temporal: loads (1) / stores (2) (main_cnt_)
   };
   Policy policy() const;
   const std::string& bcast_algo() const { return bcast_algo_; }  // "ring" | "direct"
@@ -323,6 +324,7 @@ class Engine {
   Layout L_;
   int d_ = 1;
   int f_ = 1;  // depth of the first panel (GJ_FIRST_DEPTH; default d_)
+  int main_cnt_ = 0;  // GemmExtra::c_nt of MAIN's trailing-update launches
   std::string bcast_algo_ = "ring";
   bool comm_small_tiles_ = false;  // COMM chunk-normalisation GEMMs on the small latency tile
   int bi_hint_ = -1;               // candidate-inverse kernel family (Device::set_block_inverse_hint)

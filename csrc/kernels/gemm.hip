@@ -122,6 +122,18 @@ __device__ __forceinline__ void bstore(double v, __amdgpu_buffer_rsrc_t r, int v
 __device__ __forceinline__ void bstore(float v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, voff, soff, 0);
 }
+// the same with the non-temporal cache policy when nt (GemmArgs::c_nt; a uniform branch)
+__device__ __forceinline__ double bload_c(__amdgpu_buffer_rsrc_t r, int voff, int soff, bool nt) {
+  const u32x2 v = nt ? __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 2)
+                     : __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+  return __builtin_bit_cast(double, v);
+}
+__device__ __forceinline__ void bstore_c(double v, __amdgpu_buffer_rsrc_t r, int voff, int soff, bool nt) {
+  if (nt)
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, voff, soff, 2);
+  else
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, voff, soff, 0);
+}
 
 enum { MODE_ACC = 0, MODE_STORE = 1, MODE_RESID = 2 };
 struct GemmArgs {
@@ -158,6 +170,7 @@ struct GemmArgs {
   int64_t skc0, skc1;   // GemmExtra::skip_c0 / skip_c1 (whole tiles)
   const void* cin;      // GemmExtra::c_in (MODE_ACC input array, ld ldcin; null: C itself)
   int64_t ldcin;
+  int c_nt;             // LDS-DMA fp64 kernel: C loads (bit 0) / stores (bit 1) non-temporal (GJ_GLDS_CNT)
 };
 
 // GemmExtra::rsel: physical first row of the tile whose logical first row is r (the block height
@@ -593,7 +606,7 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
           const int c = clane + j * 16;
           if (MODE == MODE_ACC) {
             const bool ok = r < Mt && c < Nt && !zrow && !(c >= z0 && c < z1);
-            acc[i][j][q] = bload<double>(rci, ok ? civoff + j * 16 * ES : kOOB, soff);
+            acc[i][j][q] = bload_c(rci, ok ? civoff + j * 16 * ES : kOOB, soff, g.c_nt & 1);
           } else {
             acc[i][j][q] = 0.0;
           }
@@ -754,7 +767,7 @@ __global__ __launch_bounds__(glds::NT, OCC) void gemm_glds_f64(GemmArgs g) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int c = clane + j * 16;
-        bstore(acc[i][j][q], rc, (r < Mt && c < Nt) ? cvoff + j * 16 * ES : kOOB, soff);
+        bstore_c(acc[i][j][q], rc, (r < Mt && c < Nt) ? cvoff + j * 16 * ES : kOOB, soff, g.c_nt & 2);
       }
     }
   if (g.tneg && n0 < g.tncols) {  // -C^T of the columns < tncols (GemmExtra::tneg)
@@ -1011,6 +1024,19 @@ void set_glds_tile(int bn) {
   g_glds_tile = bn;
 }
 
+// GemmArgs::c_nt: the fp64 LDS-DMA kernel's C loads (bit 0) / stores (bit 1) with the non-temporal
+// cache policy, per launch from GemmExtra::c_nt (-1: unnamed, 0); GJ_GLDS_CNT=<bits> forces every
+// launch (A/B runs).  N = 32768, every LDS-DMA launch, one box, two repetitions: 1129.9 / 1129.6 ms
+// (0), 1123.5 / 1121.6 (loads), 1120.3 / 1117.4 (stores), 1111.7 / 1109.8 (both) -- the C tile is
+// read and written once per panel, and streaming it leaves L2 to A and B (scripts/runs/r6_cnt.sh).
+static int glds_cnt(int per_launch) {
+  static const int forced = [] {
+    const char* e = getenv("GJ_GLDS_CNT");
+    return e ? (std::atoi(e) & 3) : -1;
+  }();
+  return forced >= 0 ? forced : per_launch > 0 ? (per_launch & 3) : 0;
+}
+
 // GJ_GLDS_GROUP=<G>: tile rows walked together per XCD (A/B runs; default 4)
 static int glds_group() {
   static const int g = [] {
@@ -1036,6 +1062,7 @@ static void launch_glds(const GemmArgs& a0, hipStream_t s) {
     const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;
     if (nwg <= 0) return;
     a.group = glds_group();
+    a.c_nt = glds_cnt(a.c_nt);
     if (build0 == 33)
       hipLaunchKernelGGL((gemm_glds_f64<MODE, 3, 3, 8, 1, 128>), dim3((unsigned)nwg), dim3(glds::NT), 0, s, a);
     else if (build0 == 32)
@@ -1058,6 +1085,7 @@ static void launch_glds(const GemmArgs& a0, hipStream_t s) {
   // the <2,3,8> schedule is the faster of the two 4-per-CU builds, so it is the only build.  Tile
   // rows are walked in groups of 4 (+0.5-1 %; groups 1-32 measured).
   a.group = 4;
+  a.c_nt = glds_cnt(a.c_nt);
   // Round 5: with the peeled loop (constant vmcnt, no per-slice address / mask VALU) the third
   // stage pays -- it lets a slice's DMA stay in flight across a whole slice of MFMAs -- so 3.3 is
   // the default at 4 workgroups per CU; under a CU reservation the 5-per-CU build (2 stages: 5 x 3
@@ -1516,6 +1544,7 @@ static void fill_extra(GemmArgs& a, const GemmExtra* ex) {
   a.dense = ex ? ex->dense : false;
   a.build = ex ? ex->glds_build : 0;
   a.tile = ex ? ex->glds_tile : 0;
+  a.c_nt = ex ? ex->c_nt : -1;
   a.rsel_m = ex ? ex->rsel_m : 0;
   a.cin = ex ? ex->c_in : nullptr;
   a.skc0 = ex ? ex->skip_c0 : 0;

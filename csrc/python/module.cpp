@@ -511,6 +511,7 @@ PYBIND11_MODULE(_C, mod) {
                                d["lat_reg"] = pl.lat_reg;
                                d["chunk_skip"] = pl.chunk_skip;
                                d["first_depth"] = pl.first_depth;
+                               d["main_cnt"] = pl.main_cnt;
                                d["bcast"] = e.eng->bcast_algo();
                                d["bcast_tuning"] = e.comm->bcast_report();
                                d["comm"] = e.comm->describe();

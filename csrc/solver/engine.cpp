@@ -285,6 +285,12 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // cost more): the MAIN merge at N = 32768 1078.2 / 1079.5 -> 1076.3 / 1075.5 ms, same box,
   // alternating (scripts/runs/r6_skip128.sh) -- on wherever that tile runs; the chunk-pass merge
   // stays with the reservation.
+  // MAIN's trailing update streams its C tile (read and written once per panel) with the
+  // non-temporal cache policy, loads and stores (GemmExtra::c_nt; GJ_MAIN_CNT=<bits> overrides):
+  // N = 32768 1129.9 / 1129.6 -> 1111.7 / 1109.8 ms with every LDS-DMA launch streaming (one box,
+  // scripts/runs/r6_cnt.sh), MAIN alone: scripts/runs/r6_cnt2.sh
+  main_cnt_ = 3;
+  if (const char* e = std::getenv("GJ_MAIN_CNT")) main_cnt_ = std::atoi(e) & 3;
   skip_cols_ = reserved_cus_ > 0 || gemm_tile_ == 128;
   if (const char* e = std::getenv("GJ_SKIP_COLS")) skip_cols_ = std::atoi(e) != 0;
   chunk_skip_ = reserved_cus_ > 0;
@@ -324,6 +330,7 @@ Engine::Policy Engine::policy() const {
   Policy p;
   p.depth = d_;
   p.first_depth = f_;
+  p.main_cnt = main_cnt_;
   p.env_overrides = env_overrides_;
   p.gemm_tile = gemm_tile_;
   p.nchunks = (int)cb0_.size();
@@ -1363,6 +1370,7 @@ void Engine::big_update(int64_t u) {
         // N = 16384 161.6 vs 164.6 ms; without a reservation the chain starves (N = 32768 1195 vs
         // 1158 ms), profiles/gemm_stall_r4.md
         ex.dense = dense_gemm_;
+        ex.c_nt = main_cnt_;
         dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, rb[z] - ra[z], K, At, rows,
                   rb_chunk(par, c) + (ra[z] - c0) * (int64_t)esz(), W, elem(X_, ra[z]), npad, ms, ex);
       }

@@ -341,3 +341,17 @@ def test_async_first_depth_and_chunk_plan_on_gpu(p, first, plan, monkeypatch):
                          jitter_us=20.0 if p > 1 else 0.0).run(n, gen="random", seed=5)
     assert base["status"] == 0 and rep["status"] == 0, (base["message"], rep["message"])
     assert rep["residual"] < 10 * base["residual"] + 1e-9, (rep["residual"], base["residual"])
+
+
+@pytest.mark.parametrize("cnt", ["0", "1", "2"])
+def test_main_nontemporal_c_bit_identical(cnt, monkeypatch):
+    """MAIN's trailing update with its C tile through the non-temporal cache policy (the default,
+    GemmExtra::c_nt = 3) and without / half of it: only the cache policy differs, so the inverse is
+    bit-identical."""
+    n, m = 3000, 128
+    A = generate_matrix(n, "random", 21)
+    a = gj.GaussJordan(block_size=m, device="gpu").inverse(A)
+    monkeypatch.setenv("GJ_MAIN_CNT", cnt)
+    b = gj.GaussJordan(block_size=m, device="gpu").inverse(A)
+    assert np.array_equal(a, b)
+    assert np.abs(a @ A - np.eye(n)).max() < 1e-8
