@@ -288,7 +288,8 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // MAIN's trailing update streams its C tile (read and written once per panel) with the
   // non-temporal cache policy, loads and stores (GemmExtra::c_nt; GJ_MAIN_CNT=<bits> overrides):
   // N = 32768 1129.9 / 1129.6 -> 1111.7 / 1109.8 ms with every LDS-DMA launch streaming (one box,
-  // scripts/runs/r6_cnt.sh), MAIN alone: scripts/runs/r6_cnt2.sh
+  // scripts/runs/r6_cnt.sh); MAIN's launches only, another box: N = 8192 23.04 -> 22.86 ms, 16384
+  // 149.2 -> 147.9 ms, 32768 1070.1 -> 1057.8 ms (scripts/runs/r6_cnt2.sh, profiles/gemm_cache_policy_r6.md)
   main_cnt_ = 3;
   if (const char* e = std::getenv("GJ_MAIN_CNT")) main_cnt_ = std::atoi(e) & 3;
   skip_cols_ = reserved_cus_ > 0 || gemm_tile_ == 128;
