@@ -123,6 +123,16 @@ __device__ __forceinline__ void bstore(float v, __amdgpu_buffer_rsrc_t r, int vo
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, voff, soff, 0);
 }
 // the same with the non-temporal cache policy when nt (GemmArgs::c_nt; a uniform branch)
+__device__ __forceinline__ float bload_c32(__amdgpu_buffer_rsrc_t r, int voff, int soff, bool nt) {
+  return __builtin_bit_cast(float, nt ? __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 2)
+                                      : __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+__device__ __forceinline__ void bstore_c(float v, __amdgpu_buffer_rsrc_t r, int voff, int soff, bool nt) {
+  if (nt)
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, voff, soff, 2);
+  else
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, voff, soff, 0);
+}
 __device__ __forceinline__ double bload_c(__amdgpu_buffer_rsrc_t r, int voff, int soff, bool nt) {
   const u32x2 v = nt ? __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 2)
                      : __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
@@ -1216,7 +1226,7 @@ __global__ __launch_bounds__(glds32::NT, OCC) void gemm_glds_f32(GemmArgs g) {
           const int c = clane + j * 32;
           if (MODE == MODE_ACC) {
             const bool ok = r < Mt && c < Nt && !zrow && !(c >= z0 && c < z1);
-            acc[i][j][q] = bload<float>(rci, ok ? civoff + j * 32 * ES : kOOB, dr * ldi * ES);
+            acc[i][j][q] = bload_c32(rci, ok ? civoff + j * 32 * ES : kOOB, dr * ldi * ES, g.c_nt & 1);
           } else {
             acc[i][j][q] = 0.0f;
           }
@@ -1348,7 +1358,7 @@ __global__ __launch_bounds__(glds32::NT, OCC) void gemm_glds_f32(GemmArgs g) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int c = clane + j * 32;
-        bstore(acc[i][j][q], rc, (r < Mt && c < Nt) ? cvoff + j * 32 * ES : kOOB, dr * ldc * ES);
+        bstore_c(acc[i][j][q], rc, (r < Mt && c < Nt) ? cvoff + j * 32 * ES : kOOB, dr * ldc * ES, g.c_nt & 2);
       }
     }
 }
@@ -1364,6 +1374,7 @@ static void launch_glds32(const GemmArgs& a0, hipStream_t s) {
     const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;
     if (nwg <= 0) return;
     a.group = 4;
+    a.c_nt = glds_cnt(a.c_nt);
     hipLaunchKernelGGL((gemm_glds_f32<MODE, 2, 3, 16, 1, 256>), dim3((unsigned)nwg), dim3(glds32::NT), 0, s, a);
     return;
   }
@@ -1372,6 +1383,7 @@ static void launch_glds32(const GemmArgs& a0, hipStream_t s) {
   const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;
   if (nwg <= 0) return;
   a.group = 4;
+  a.c_nt = glds_cnt(a.c_nt);
   // <stages, launch-bounds workgroups per CU, slice depth>; 8 KiB of LDS per 8 k rows.  Measured
   // (round 2, TF/s at 32768x16384x512 / 16384x65536x512 / 4096x65536x1024): <2,3,16>
   // 125.9 / 128.5 / 132.4 (4 WG/CU at 114 VGPRs), <2,2,16> 122.1 / 128.1 / 133.1, <3,2,16> 122.5 /

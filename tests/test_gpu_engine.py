@@ -343,15 +343,15 @@ def test_async_first_depth_and_chunk_plan_on_gpu(p, first, plan, monkeypatch):
     assert rep["residual"] < 10 * base["residual"] + 1e-9, (rep["residual"], base["residual"])
 
 
-@pytest.mark.parametrize("cnt", ["0", "1", "2"])
-def test_main_nontemporal_c_bit_identical(cnt, monkeypatch):
+@pytest.mark.parametrize("dtype,cnt", [("fp64", "0"), ("fp64", "1"), ("fp64", "2"), ("fp32", "0")])
+def test_main_nontemporal_c_bit_identical(dtype, cnt, monkeypatch):
     """MAIN's trailing update with its C tile through the non-temporal cache policy (the default,
-    GemmExtra::c_nt = 3) and without / half of it: only the cache policy differs, so the inverse is
-    bit-identical."""
+    GemmExtra::c_nt = 3; fp64 and fp32 LDS-DMA kernels) and without / half of it: only the cache
+    policy differs, so the inverse is bit-identical."""
     n, m = 3000, 128
-    A = generate_matrix(n, "random", 21)
-    a = gj.GaussJordan(block_size=m, device="gpu").inverse(A)
+    A = generate_matrix(n, "random" if dtype == "fp64" else "randshift", 21)
+    a = gj.GaussJordan(block_size=m, device="gpu", dtype=dtype).inverse(A)
     monkeypatch.setenv("GJ_MAIN_CNT", cnt)
-    b = gj.GaussJordan(block_size=m, device="gpu").inverse(A)
+    b = gj.GaussJordan(block_size=m, device="gpu", dtype=dtype).inverse(A)
     assert np.array_equal(a, b)
-    assert np.abs(a @ A - np.eye(n)).max() < 1e-8
+    assert np.abs(a @ A - np.eye(n)).max() < (1e-8 if dtype == "fp64" else 1e-3)
