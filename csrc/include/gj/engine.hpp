@@ -325,6 +325,7 @@ class Engine {
   int d_ = 1;
   int f_ = 1;  // depth of the first panel (GJ_FIRST_DEPTH; default d_)
   int main_cnt_ = 0;  // GemmExtra::c_nt of MAIN's trailing-update launches
+  int main_split_ = 0;  // GJ_MAIN_SPLIT: MAIN's chunk launches in two column halves (1 first, 2 all)
   std::string bcast_algo_ = "ring";
   bool comm_small_tiles_ = false;  // COMM chunk-normalisation GEMMs on the small latency tile
   int bi_hint_ = -1;               // candidate-inverse kernel family (Device::set_block_inverse_hint)

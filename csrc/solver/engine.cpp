@@ -292,6 +292,7 @@ Engine::Engine(Device& dev, Comm& comm, int64_t n, int64_t m, const SolveOptions
   // 149.2 -> 147.9 ms, 32768 1070.1 -> 1057.8 ms (scripts/runs/r6_cnt2.sh, profiles/gemm_cache_policy_r6.md)
   main_cnt_ = 3;
   if (const char* e = std::getenv("GJ_MAIN_CNT")) main_cnt_ = std::atoi(e) & 3;
+  if (const char* e = std::getenv("GJ_MAIN_SPLIT")) main_split_ = std::atoi(e);
   skip_cols_ = reserved_cus_ > 0 || gemm_tile_ == 128;
   if (const char* e = std::getenv("GJ_SKIP_COLS")) skip_cols_ = std::atoi(e) != 0;
   chunk_skip_ = reserved_cus_ > 0;
@@ -1360,20 +1361,35 @@ void Engine::big_update(int64_t u) {
     } else {
       ra[0] = c0; rb[0] = c1; nr = 1;
     }
+    // GJ_MAIN_SPLIT (A/B): the chunk's launch in two column halves -- 1: the panel's first chunk
+    // only, 2: every chunk -- an extra launch boundary where a drained CU can take the pivot
+    // chain's candidate inverse (profiles/rocprof_n32768_r6_final.md)
+    const int pieces = (main_split_ == 2 || (main_split_ == 1 && i == 0)) ? 2 : 1;
+    const int64_t s_abs0 = c0 + sk0, s_abs1 = c0 + sk1;  // skipped columns (absolute; empty if equal)
     if (rows > 0)
       for (int64_t z = 0; z < nr; ++z) {
-        GemmExtra ex = prows;
-        ex.skip_c0 = sk0;
-        ex.skip_c1 = sk1;
-        ex.zc0 = pc0 - ra[z];  // the panel's own block columns enter as 0
-        ex.zc1 = pc1 - ra[z];
-        // with CUs reserved for the pivot chain the trailing update may fill the rest densely:
-        // N = 16384 161.6 vs 164.6 ms; without a reservation the chain starves (N = 32768 1195 vs
-        // 1158 ms), profiles/gemm_stall_r4.md
-        ex.dense = dense_gemm_;
-        ex.c_nt = main_cnt_;
-        dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, rb[z] - ra[z], K, At, rows,
-                  rb_chunk(par, c) + (ra[z] - c0) * (int64_t)esz(), W, elem(X_, ra[z]), npad, ms, ex);
+        int64_t cut[3] = {ra[z], rb[z], rb[z]};
+        int np = 1;
+        if (pieces == 2 && rb[z] - ra[z] >= 256) {
+          cut[1] = ra[z] + ((rb[z] - ra[z]) / 256) * 128;  // tile-aligned (128) from the range's start
+          np = 2;
+        }
+        for (int h = 0; h < np; ++h) {
+          const int64_t a = cut[h], b = cut[h + 1];
+          GemmExtra ex = prows;
+          const int64_t s0 = std::max(s_abs0, a), s1 = std::min(s_abs1, b);
+          ex.skip_c0 = s1 > s0 ? s0 - a : 0;
+          ex.skip_c1 = s1 > s0 ? s1 - a : 0;
+          ex.zc0 = pc0 - a;  // the panel's own block columns enter as 0
+          ex.zc1 = pc1 - a;
+          // with CUs reserved for the pivot chain the trailing update may fill the rest densely:
+          // N = 16384 161.6 vs 164.6 ms; without a reservation the chain starves (N = 32768 1195 vs
+          // 1158 ms), profiles/gemm_stall_r4.md
+          ex.dense = dense_gemm_;
+          ex.c_nt = main_cnt_;
+          dev_.gemm(opt_.dtype, GemmOp::Acc, ALayout::KMajor, rows, b - a, K, At, rows,
+                    rb_chunk(par, c) + (a - c0) * (int64_t)esz(), W, elem(X_, a), npad, ms, ex);
+        }
       }
     prof_end(PH_UPDATE, pe, ms);
     if (i + 1 == C && vlocal_on()) vlocal_hash(u, V_LE, true, ms);  // ... and after the last one

@@ -282,3 +282,18 @@ def test_shallow_first_panel_chunk_plan(monkeypatch):
     monkeypatch.setenv("GJ_CHUNK_PLAN", "6,10,4")
     with pytest.raises(Exception, match="GJ_CHUNK_PLAN"):
         gj.GaussJordan(block_size=8, device="cpu", depth=2).inverse(A)
+
+
+@pytest.mark.parametrize("split", ["1", "2"])
+@pytest.mark.parametrize("skip", ["0", "1"])
+@pytest.mark.parametrize("ranks", [1, 3])
+def test_main_split_launches_bit_identical(monkeypatch, split, skip, ranks):
+    # GJ_MAIN_SPLIT: MAIN's chunk updates in two column halves (with and without the look-ahead
+    # skip inside one launch): the same products per element, so the same bits
+    A = _mat("rand", 1100, 13)
+    monkeypatch.setenv("GJ_SKIP_COLS", skip)
+    a = gj.GaussJordan(block_size=10, ranks=ranks, device="cpu", depth=4, chunk_cols=600).inverse(A)
+    monkeypatch.setenv("GJ_MAIN_SPLIT", split)
+    b = gj.GaussJordan(block_size=10, ranks=ranks, device="cpu", depth=4, chunk_cols=600).inverse(A)
+    assert np.array_equal(a, b)
+    assert np.abs(a @ A - np.eye(1100)).max() < 1e-8
