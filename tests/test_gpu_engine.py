@@ -166,17 +166,11 @@ def test_device_resident_fp32_solve_is_refined(k):
     assert np.abs(x.double().cpu().numpy() - xr).max() / np.abs(xr).max() < 1e-6
 
 
-# p = 8 asynchronous ranks at an explicit depth 2 is the configuration of the round-3 wrong inverse,
-# never localised; the final round-6 build fails this case in 5 of 8 standalone runs (with and
-# without the non-temporal C tile), once with GJ_VERIFY naming the buffer: "step 12 (panel 6),
-# phase trailing update, buffer Rb[0] chunk 1 segment 0, root rank 3: rank(s) [7] consumed
-# different bytes on stream MAIN" (profiles/verify_r6.md, scripts/runs/r6_p8d2.sh).  Depth 2 is not
-# the default at p > 1 (4 / 8 are).  Kept as a non-strict xfail so the tier records it.
-_P8D2 = pytest.param(8, "async", 2, marks=pytest.mark.xfail(
-    strict=False, reason="intermittent wrong inverse at p = 8, depth 2, async ranks (round-3 failure class)"))
-
-
-@pytest.mark.parametrize("p,comm,depth", [(1, "auto", 2), (1, "auto", 4), (3, "async", 4), _P8D2])
+# p = 8 asynchronous ranks at an explicit depth 2: the deferred updates on MAIN (GJ_SPLIT=2) gave
+# intermittent wrong inverses there on the final round-6 build (profiles/verify_r6.md); the engine
+# refuses that variant on the GPU at p > 1, so p > 1 checks split 0 / 1 and the latency-kernel
+# choice only (split 2 stays covered at p = 1 here and at every p on the host executor).
+@pytest.mark.parametrize("p,comm,depth", [(1, "auto", 2), (1, "auto", 4), (3, "async", 4), (8, "async", 2)])
 def test_split_column_updates_bit_identical_on_gpu(p, comm, depth, monkeypatch, native):
     """Engine::split_ on the GPU: the chain's row-selected look-ahead / column updates (GemmExtra::rsel,
     LDS-DMA kernel for 128-row blocks) plus the deferred ones on COMM (1) or MAIN (2) give the
@@ -185,7 +179,10 @@ def test_split_column_updates_bit_identical_on_gpu(p, comm, depth, monkeypatch, 
     n, m = 2560, 128
     A = generate_matrix(n, "random", 21)[::-1].copy()
     out = []
-    for split, lat in (("0", "0"), ("1", "0"), ("2", "0"), ("0", "1"), ("2", "1")):
+    variants = (("0", "0"), ("1", "0"), ("2", "0"), ("0", "1"), ("2", "1"))
+    if p > 1:
+        variants = tuple(v for v in variants if v[0] != "2")
+    for split, lat in variants:
         monkeypatch.setenv("GJ_SPLIT", split)
         monkeypatch.setenv("GJ_LAT_GLDS", lat)  # the engine's choice (GemmExtra::lat_wide) ...
         native.set_lat_glds(lat == "1")         # ... and every other latency launch
@@ -194,7 +191,7 @@ def test_split_column_updates_bit_identical_on_gpu(p, comm, depth, monkeypatch, 
                                       jitter_us=30.0 if comm == "async" else 0.0).inverse(A))
         finally:
             native.set_lat_glds(False)
-    names = ["split 1", "split 2", "lat_glds", "split 2 + lat_glds"]
+    names = [("split %s" % sp) + (" + lat_glds" if lat == "1" else "") for sp, lat in variants[1:]]
     ref = np.linalg.inv(A)
     errs = {"split 0": np.abs(out[0] - ref).max() / np.abs(ref).max()}
     for name, o in zip(names, out[1:]):
@@ -203,6 +200,10 @@ def test_split_column_updates_bit_identical_on_gpu(p, comm, depth, monkeypatch, 
         assert np.array_equal(out[0], o), f"{name} differs from split 0: max |diff| " \
             f"{np.abs(out[0] - o).max():.3e}; error vs numpy per variant {errs}"
     assert errs["split 1"] < 1e-8
+    if p > 1:
+        monkeypatch.setenv("GJ_SPLIT", "2")
+        with pytest.raises(Exception, match="GJ_SPLIT=2"):
+            gj.GaussJordan(block_size=m, ranks=p, device="gpu", comm=comm, depth=depth).inverse(A)
 
 
 @pytest.mark.parametrize("p", [3, 8])
